@@ -1,0 +1,386 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Runs only in the development container, where /root/reference exists:
+
+    python tests/golden/make_golden.py
+
+It imports the unmodified ryannduma/chemeleon sources from /root/reference
+(by path; no file there is copied or written: bytecode writing is disabled)
+under small import shims that stand in for third-party packages missing from
+this image (torch_geometric, pytorch_lightning, torchmetrics, ase, wandb,
+transformers class names). The shims only reproduce what the hot path uses:
+
+* torch_geometric.utils.dense_to_sparse: row-major nonzero of a 2-D adjacency,
+  as PyG does;
+* torch_geometric.data.Data / Batch.from_data_list: node->graph vector,
+  `natoms` concatenated into a [B] tensor, num_nodes / num_graphs;
+* pytorch_lightning.LightningModule: nn.Module + save_hyperparameters + device;
+* ase.Atoms / ase.build.tools.sort: numbers, cell, scaled positions, stable
+  sort by chemical symbol.
+
+The text encoder (BERT + CrystalCLIP) cannot run offline; the model is built
+with text_guide=False, then the decoder is replaced by a CSPNet with
+text_dim=512 and `text_encoder.get_text_embeds` returns the fixed seeded
+cond / null vectors of `chemeleon_amd.synthetic.synthetic_text_embeds`:
+exactly the hot path's input (north star: "computed once on host").
+
+Decoder weights come from `chemeleon_amd.synthetic` (seeded recipe) and are
+regenerated identically wherever the fixtures are used; a checksum of them is
+stored in every fixture.
+"""
+
+import os
+import sys
+import types
+import zlib
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("CHEMELEON_REFERENCE", "/root/reference")
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+from chemeleon_amd.config import default_config  # noqa: E402
+from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds  # noqa: E402
+from chemeleon_amd.synthetic import weights_crc as _crc  # noqa: E402
+
+# Z -> symbol for Z = 0..103 (0 = dummy 'X', as ase.data.chemical_symbols)
+SYMBOLS = (
+    "X H He Li Be B C N O F Ne Na Mg Al Si P S Cl Ar K Ca Sc Ti V Cr Mn Fe Co Ni Cu Zn Ga Ge As Se "
+    "Br Kr Rb Sr Y Zr Nb Mo Tc Ru Rh Pd Ag Cd In Sn Sb Te I Xe Cs Ba La Ce Pr Nd Pm Sm Eu Gd Tb Dy Ho "
+    "Er Tm Yb Lu Hf Ta W Re Os Ir Pt Au Hg Tl Pb Bi Po At Rn Fr Ra Ac Th Pa U Np Pu Am Cm Bk Cf Es Fm "
+    "Md No Lr"
+).split()
+
+
+def _install_shims():
+    def mod(name):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+        return m
+
+    # torch_geometric
+    tg = mod("torch_geometric")
+    tgu = mod("torch_geometric.utils")
+    tgd = mod("torch_geometric.data")
+    tg.utils, tg.data = tgu, tgd
+
+    def dense_to_sparse(adj):
+        idx = adj.nonzero().t().contiguous()
+        return idx, adj[idx[0], idx[1]]
+
+    tgu.dense_to_sparse = dense_to_sparse
+
+    class Data:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+    class Batch:
+        @classmethod
+        def from_data_list(cls, dl):
+            b = cls()
+            ns = [d.x.shape[0] for d in dl]
+            b.batch = torch.arange(len(dl)).repeat_interleave(torch.tensor(ns))
+            b.natoms = torch.tensor([d.natoms for d in dl])
+            b.num_nodes = sum(ns)
+            b.num_graphs = len(dl)
+            return b
+
+        def to(self, device):
+            return self
+
+    tgd.Data, tgd.Batch = Data, Batch
+
+    # pytorch_lightning
+    pl = mod("pytorch_lightning")
+
+    class LightningModule(nn.Module):
+        def save_hyperparameters(self, *a, **k):
+            self.hparams = a[0] if a else {}
+
+        @property
+        def device(self):
+            return torch.device("cpu")
+
+    pl.LightningModule = LightningModule
+    tm = mod("torchmetrics")
+    tm.MeanAbsoluteError = type("MeanAbsoluteError", (nn.Module,), {})
+
+    # ase
+    ase = mod("ase")
+    ab = mod("ase.build")
+    abt = mod("ase.build.tools")
+    ase.build, ab.tools = ab, abt
+
+    class Atoms:
+        def __init__(self, numbers=None, cell=None, pbc=None):
+            self.numbers = np.asarray(numbers)
+            self.cell = np.asarray(cell)
+            self.pbc = pbc
+            self.scaled = np.zeros((len(self.numbers), 3), np.float32)
+
+        def set_scaled_positions(self, p):
+            self.scaled = np.asarray(p)
+
+        def get_chemical_symbols(self):
+            return [SYMBOLS[int(z)] for z in self.numbers]
+
+        def __getitem__(self, idx):
+            a = Atoms(self.numbers[idx], self.cell, self.pbc)
+            a.scaled = self.scaled[idx]
+            return a
+
+    def sort(atoms, tags=None):
+        tags = atoms.get_chemical_symbols() if tags is None else list(tags)
+        deco = sorted([(tag, i) for i, tag in enumerate(tags)])
+        return atoms[[i for _, i in deco]]
+
+    ase.Atoms, abt.sort = Atoms, sort
+    mod("wandb")
+    tr = mod("transformers")
+    for n in ["BertModel", "BertTokenizer", "T5EncoderModel", "T5Tokenizer", "AutoTokenizer", "AutoModelForCausalLM"]:
+        setattr(tr, n, type(n, (), {}))
+
+
+def load_reference():
+    _install_shims()
+    sys.path.insert(0, REF)
+    import chemeleon.modules.chemeleon as chm  # noqa: E402
+    import chemeleon.modules.cspnet as csp  # noqa: E402
+    import chemeleon.utils.diff_utils as du  # noqa: E402
+    import chemeleon.utils.scatter as sc  # noqa: E402
+    return chm, csp, du, sc
+
+
+class StubTextEncoder(nn.Module):
+    def __init__(self, cond, null):
+        super().__init__()
+        self.cond, self.null = cond, null
+
+    def get_text_embeds(self, texts, cond_drop_prob, device):
+        v = self.cond if cond_drop_prob == 0.0 else self.null
+        return v.expand(len(texts), -1).clone()
+
+
+def build_reference_model(chm, csp, T, seed_sched=0):
+    cfg = default_config()
+    cfg["timesteps"] = T
+    cfg["text_guide"] = False
+    torch.manual_seed(seed_sched)  # sigmas_norm Monte-Carlo draws
+    m = chm.Chemeleon(cfg)
+    m.text_guide = True
+    dec = csp.CSPNet(hidden_dim=512, time_dim=128, text_dim=512, num_layers=6, max_atoms=104, act_fn="silu",
+                     dis_emb="sin", num_freqs=128, edge_style="fc", cutoff=6.0, max_neighbors=20, ln=True,
+                     ip=True, smooth=False, pred_atom_types=True)
+    sd = synthetic_state_dict(default_config())
+    dec.load_state_dict(sd)
+    m.decoder = dec.eval()
+    cond, null = synthetic_text_embeds(512)
+    m.text_encoder = StubTextEncoder(cond, null)
+    return m, sd
+
+
+def weights_crc(sd):
+    return np.int64(_crc(sd))
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: (v.numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in arrs.items()})
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def gen_schedules(chm, csp):
+    for T in (100, 1000):
+        m, _ = build_reference_model(chm, csp, T)
+        b, s, d = m.beta_scheduler, m.sigma_scheduler, m.d3pm
+        ts = [1, 2, T // 2, T - 1, T]
+        save(f"schedules_T{T}.npz", betas=b.betas, alphas=b.alphas, alphas_cumprod=b.alphas_cumprod,
+             beta_sigmas=b.sigmas, sigmas=s.sigmas, sigmas_norm=s.sigmas_norm, qmat_t=np.array(ts),
+             q_mats=d.q_mats[ts], q_one_step=d.q_one_step_mats[ts])
+
+
+def gen_units(chm, csp, du, sc):
+    g = torch.Generator().manual_seed(11)
+    out = {}
+    # torch remainder edge cases (cspnet.py:324, chemeleon.py:462)
+    x = torch.tensor([-1e-9, -0.3, 1.7, 0.0, -0.0, 2.0, 0.9999999, -1.0000001, 3.25, -7.5e-8, 1e-30, -2.5])
+    out["mod_in"], out["mod_out"] = x, x % 1.0
+    # Fourier features (cspnet.py:38-52)
+    fd = torch.rand(64, 3, generator=g)
+    fd[0] = torch.tensor([0.0, 1.0, 0.99999994])
+    out["fourier_in"], out["fourier_out"] = fd, csp.SinusoidsEmbedding(n_frequencies=128)(fd)
+    # time embedding (cspnet.py:21-35)
+    tt = torch.tensor([1, 2, 3, 17, 250, 500, 999, 1000])
+    out["temb_in"], out["temb_out"] = tt, csp.SinusoidalTimeEmbeddings(128)(tt)
+    # scatter_mean (scatter.py:88-112), including an empty segment
+    src = torch.randn(10, 7, generator=g)
+    idx = torch.tensor([0, 0, 1, 3, 3, 3, 4, 4, 4, 4])
+    out["scatter_src"], out["scatter_idx"], out["scatter_out"] = src, idx, sc.scatter_mean(src, idx, dim=0, dim_size=6)
+    # D3PM p_logits (diff_utils.py:307-329) at T=100 at edge timesteps
+    m, _ = build_reference_model(chm, csp, 100)
+    n = 48
+    t_node = torch.tensor([100, 99, 50, 2, 1, 1] * 8)
+    xt = torch.randint(0, 104, (n,), generator=g)
+    xt[::3] = 0
+    logits = torch.randn(n, 104, generator=g) * 3
+    u = torch.rand(n, 104, generator=g)
+    u[0, :5] = torch.tensor([0.0, 1e-9, 1.0, 0.5, 1e-6])
+    out["d3pm_t"], out["d3pm_xt"], out["d3pm_logits"], out["d3pm_u"] = t_node, xt, logits, u
+    out["d3pm_post"] = m.d3pm.q_posterior_logits(logits, xt, t_node, is_x_0_one_hot=True)
+    out["d3pm_out"] = m.d3pm.p_logits(logits, xt, t_node, u)
+    save("units.npz", **out)
+
+
+def _decoder_case(m, sd, natoms, seed, t):
+    g = torch.Generator().manual_seed(seed)
+    B, N = len(natoms), sum(natoms)
+    nat = torch.tensor(natoms)
+    n2g = torch.arange(B).repeat_interleave(nat)
+    a = torch.randint(0, 104, (N,), generator=g)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.randn(B, 3, 3, generator=g) * 2.0
+    te = m.time_embed(torch.full((B,), t, dtype=torch.long))
+    cond, null = synthetic_text_embeds(512)
+    text = cond.expand(B, -1)
+    hid = []
+    dec = m.decoder
+    # capture per-layer node features through forward hooks on the CSP layers
+    hooks = [dec._modules[f"csp_layer_{i}"].register_forward_hook(lambda mod, i_, o: hid.append(o.detach().clone()))
+             for i in range(6)]
+    with torch.no_grad():
+        o = dec(atom_types=a, frac_coords=x, lattices=lat, num_atoms=nat, node2graph=n2g, t=te, text_embeds=text)
+        for h in hooks:
+            h.remove()
+        mp = m.model_predictions(te, a, x, lat, nat, n2g, 2.0, cond.expand(B, -1), null.expand(B, -1))
+    return dict(natoms=nat, atom_types=a, frac=x, lattices=lat, t=np.int64(t), types=o.atom_types_out,
+                lattice_out=o.lattice_out, coords=o.coords_out, node_features=o.node_features,
+                hidden=torch.stack(hid, 0), cfg_types=mp[0], cfg_lattice=mp[1], cfg_coords=mp[2],
+                weights_crc=weights_crc(sd))
+
+
+def gen_decoder(chm, csp):
+    m, sd = build_reference_model(chm, csp, 1000)
+    save("decoder_4x6.npz", **_decoder_case(m, sd, [6, 6, 6, 6], 21, 700))
+    save("decoder_ragged.npz", **_decoder_case(m, sd, [3, 5, 8, 1], 22, 37))
+
+
+def gen_single_steps(chm, csp):
+    """Teacher-forced single steps: a state at t (from a short reference run
+    or synthetic), seeded noise, one reference reverse step -> state at t-1.
+    The step is driven through the reference's own `_sample_generator` by
+    patching its trajectory container, so the reference code is what runs."""
+    T = 1000
+    m, sd = build_reference_model(chm, csp, T)
+    for tag, natoms, ts in (("64x20", [20] * 64, [1000, 999, 500, 2, 1]), ("16x40", [40] * 16, [1000, 500, 1])):
+        B, N = len(natoms), sum(natoms)
+        rec = {"natoms": torch.tensor(natoms), "ts": np.array(ts), "weights_crc": weights_crc(sd)}
+        for t in ts:
+            g = torch.Generator().manual_seed(1000 + t)
+            a = torch.randint(0, 104, (N,), generator=g)
+            a[::4] = 0
+            x = torch.rand(N, 3, generator=g)
+            lat = torch.randn(B, 3, 3, generator=g) * 3.0 * torch.tensor([[1, 0, 1], [1, 1, 1], [0, 0, 1]])
+            nxt = reference_single_step(m, natoms, a, x, lat, t, noise_seed=5000 + t)
+            rec[f"t{t}_a"], rec[f"t{t}_x"], rec[f"t{t}_l"] = a, x, lat
+            rec[f"t{t}_a_out"], rec[f"t{t}_x_out"], rec[f"t{t}_l_out"] = nxt
+        save(f"step_{tag}.npz", **rec)
+
+
+def reference_single_step(m, natoms, a, x, lat, t, noise_seed):
+    """Run the reference generator for exactly one step at time t from the
+    given state. The loop iterator (`tqdm(range(T, 0, -1))`,
+    chemeleon.py:379) is replaced by one that yields only t, and the state at
+    t is planted in the trajectory container; `time_start` stays T, so the
+    t == T lattice clip (:424) behaves as in a full run. The CPU global
+    generator is seeded with noise_seed right after the initial noise draw,
+    so rand_a, rand_l, rand_x, rand_x come from that seed in the reference's
+    order."""
+    import chemeleon.modules.chemeleon as chm
+    from chemeleon.modules import schema
+    T0 = m.beta_scheduler.timesteps
+    orig_set = schema.TrajectoryContainer.__setitem__
+    orig_get = schema.TrajectoryContainer.get_atoms
+    orig_tqdm = chm.tqdm
+    planted = {"done": False}
+    captured = {}
+
+    def setitem(self, key, step):
+        orig_set(self, key, step)
+        if key == T0 and not planted["done"]:
+            planted["done"] = True
+            st = schema.TrajectoryStep(num_atoms=step.num_atoms, atom_types=a.clone(), frac_coords=x.clone(),
+                                       lattices=lat.clone(), batch_idx=step.batch_idx)
+            orig_set(self, t, st)
+            torch.manual_seed(noise_seed)
+
+    def get_atoms(self, t=0, idx=None):
+        st = self[t]
+        captured["s"] = (st.atom_types.clone(), st.frac_coords.clone(), st.lattices.clone())
+        return []
+
+    schema.TrajectoryContainer.__setitem__ = setitem
+    schema.TrajectoryContainer.get_atoms = get_atoms
+    chm.tqdm = lambda it: iter([t])
+    try:
+        for _ in m._sample_generator(natoms, ["x"] * len(natoms), 2.0, 1e-5):
+            pass
+    finally:
+        schema.TrajectoryContainer.__setitem__ = orig_set
+        schema.TrajectoryContainer.get_atoms = orig_get
+        chm.tqdm = orig_tqdm
+    return captured["s"]
+
+
+def gen_trajectory(chm, csp):
+    """C0: 4 x 6 atoms, T = 100, seed 42, full reference sampler."""
+    m, sd = build_reference_model(chm, csp, 100)
+    from chemeleon.modules import schema
+    states = []
+    orig_get = schema.TrajectoryContainer.get_atoms
+
+    def get_atoms(self, t=0, idx=None):
+        st = self[t]
+        states.append((st.atom_types.clone(), st.frac_coords.clone(), st.lattices.clone()))
+        return orig_get(self, t, idx)
+
+    schema.TrajectoryContainer.get_atoms = get_atoms
+    try:
+        torch.manual_seed(42)
+        gen = m._sample_generator([6] * 4, ["Li1 Mn1 O4"] * 4, 2.0, 1e-5)
+        last = None
+        for last in gen:
+            pass
+    finally:
+        schema.TrajectoryContainer.get_atoms = orig_get
+    a = torch.stack([s[0] for s in states])
+    x = torch.stack([s[1] for s in states])
+    lat = torch.stack([s[2] for s in states])
+    # G6: ase-sorted output ordering of the final structures
+    order_numbers = np.concatenate([at.numbers for at in last])
+    order_scaled = np.concatenate([at.scaled for at in last])
+    save("trajectory_4x6_T100.npz", atom_types=a, frac=x, lattices=lat, final_sorted_numbers=order_numbers,
+         final_sorted_scaled=order_scaled, weights_crc=weights_crc(sd))
+
+
+if __name__ == "__main__":
+    if not os.path.isdir(os.path.join(REF, "chemeleon")):
+        print("reference not present; nothing to do")
+        sys.exit(0)
+    torch.set_num_threads(8)
+    chm, csp, du, sc = load_reference()
+    which = sys.argv[1:] or ["schedules", "units", "decoder", "steps", "trajectory"]
+    if "schedules" in which:
+        gen_schedules(chm, csp)
+    if "units" in which:
+        gen_units(chm, csp, du, sc)
+    if "decoder" in which:
+        gen_decoder(chm, csp)
+    if "steps" in which:
+        gen_single_steps(chm, csp)
+    if "trajectory" in which:
+        gen_trajectory(chm, csp)
