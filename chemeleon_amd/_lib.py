@@ -1,0 +1,106 @@
+"""ctypes binding of libchemeleon_hip.so (the C ABI in include/chemeleon_hip.h).
+
+The HIP library is the only compute path of this package: if it is missing,
+or a tensor is not on a HIP device, calls raise instead of falling back to a
+CPU implementation.
+"""
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CHM_LIB", os.path.join(_HERE, "lib", "libchemeleon_hip.so"))
+
+_lock = threading.Lock()
+_lib = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_float = ctypes.c_float
+
+
+class chm_dims(ctypes.Structure):
+    _fields_ = [("hidden_dim", c_int), ("time_dim", c_int), ("text_dim", c_int), ("num_layers", c_int),
+                ("max_atoms", c_int), ("num_freqs", c_int)]
+
+
+class chm_schedule(ctypes.Structure):
+    _fields_ = [("T", c_int), ("d_coef", c_void_p), ("d_time_emb", c_void_p), ("d_q_one_step", c_void_p),
+                ("d_q_mats", c_void_p)]
+
+
+# name -> (restype, argtypes); every symbol declared in include/chemeleon_hip.h
+SIGNATURES = {
+    "chm_last_error": (ctypes.c_char_p, []),
+    "chm_version": (ctypes.c_char_p, []),
+    "chm_num_params": (c_int, [ctypes.POINTER(chm_dims)]),
+    "chm_model_create": (c_int, [ctypes.POINTER(chm_dims), ctypes.POINTER(c_void_p), c_int, c_void_p,
+                                 ctypes.POINTER(c_void_p)]),
+    "chm_model_destroy": (None, [c_void_p]),
+    "chm_batch_create": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "chm_batch_destroy": (None, [c_void_p]),
+    "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
+    "chm_batch_num_nodes": (c_i64, [c_void_p]),
+    "chm_batch_num_edges": (c_i64, [c_void_p]),
+    "chm_decoder_forward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "chm_sample_step": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_u64, c_i64, c_i64,
+                                c_void_p]),
+    "chm_segment_mean": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "chm_d3pm_sample": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p]),
+    "chm_edge_features": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+
+def load(path: str = None):
+    """Load (once) and return the ctypes library. Raises loudly if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ImportError(
+                f"chemeleon_amd: HIP library not found at {p}. Build it with `python -m chemeleon_amd.build` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().chm_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None)."""
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("chemeleon_amd runs on a HIP device only: got a CPU tensor (no CPU fallback)")
+        if not t.is_contiguous():
+            raise RuntimeError("chemeleon_amd expects contiguous tensors")

@@ -1,0 +1,70 @@
+// Internal declarations shared by kernels.hip and runtime.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace chm {
+
+constexpr int H = 512;       // hidden_dim (the build implements the shipped config)
+constexpr int NF = 128;      // num_freqs
+constexpr int FD = 6 * NF;   // Fourier feature width, 768
+constexpr int TD = 128;      // time_dim
+constexpr int HEADS_N = 128; // type_out (A <= 125) + coord_out (3) packed, padded
+
+// C[M,N] = epi(A[M,K] . W[N,K]^T), fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32.
+struct GemmArgs {
+  long M;
+  int N, K;
+  const float* A; long lda;
+  const float* A2; long lda2; int ksplit;  // columns k >= ksplit come from A2[:, k - ksplit]
+  const float* W; long ldw;                // [N][K] row-major (nn.Linear layout)
+  float* C; long ldc;
+  const float* bias;                       // [N] or null
+  const float* R; long ldr;                // residual added after the activation, or null
+  const int* row2g; long gb_rowmod; const float* gb; long ldgb; int gb_cols;  // per-graph row bias
+  int act;                                 // 0 = identity, 1 = SiLU
+  // EPI_EDGE: S[c][e][n] = silu(acc + PQ[c*N + ei[e]][n] + PQ[c*N + ej[e]][H + n])
+  const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
+};
+
+enum { EPI_STD = 0, EPI_EDGE = 1 };
+
+hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
+
+hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* F, hipStream_t s);
+hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,
+                        const int* natoms, long N, long E, int P, hipStream_t s);
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s);
+hipError_t build_cond_in(const float* temb, int tstride, const float* text0, const float* text1, int text_dim, float* cin,
+                         int B, int P, hipStream_t s);
+hipError_t graph_bias(const float* lat, const float* Wc, long ldwc, const float* b1, float* out, int B, hipStream_t s);
+hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
+                   const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s);
+hipError_t layer_norm(const float* X, float* Y, long rows, const float* w, const float* b, hipStream_t s);
+hipError_t graph_heads(const float* Hf, const float* Wlat, const float* lat, const int* node_off, const int* natoms,
+                       long N, int B, int P, float* lat_out, hipStream_t s);
+hipError_t split_heads(const float* HO, long rows, int A, float* types, float* coords, hipStream_t s);
+hipError_t copy_rows(const float* src, long ld_src, float* dst, long ld_dst, long rows, int cols, hipStream_t s);
+
+struct StepArgs {
+  int t, T, A;
+  long N; int B;
+  float cs_null, cs_cond;          // (1 - s), s
+  const float* coef;               // [T+1][8]
+  const float* q_one_step;         // [T+1][A][A]
+  const float* q_mats;             // [T+1][A][A]
+  const float* HO;                 // [2][N][HEADS_N] cond then null
+  const float* LAT;                // [2][B][9]
+  int64_t* a; float* x; float* l;
+  const int* n2g;
+  const float *ra, *rl, *rx1, *rx2;  // host noise or null
+  uint64_t seed; int64_t node_base, graph_base;
+};
+hipError_t step_predictor(const StepArgs& a, hipStream_t s);
+hipError_t step_corrector(const StepArgs& a, hipStream_t s);
+hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits, const float* logits2,
+                       float w1, float w2, const int64_t* xt, const int64_t* tnode, int t_const, const float* noise,
+                       const float* q1, const float* qm, int64_t* out, uint64_t seed, int64_t node_base,
+                       hipStream_t s);
+
+}  // namespace chm

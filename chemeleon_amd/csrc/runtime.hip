@@ -1,0 +1,435 @@
+// Host runtime + C ABI (include/chemeleon_hip.h) of the Chemeleon sampling path.
+//
+// chm_model  : packed device copy of the CSPNet decoder weights.
+// chm_batch  : one (ragged) batch of crystals: index tables of the implicit
+//              fully connected edge layout + the decoder workspace, all
+//              allocated once at creation. Decoder calls and sampler steps
+//              allocate nothing, synchronise nothing and are capturable.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/chemeleon_hip.h"
+#include "chm_internal.h"
+
+using namespace chm;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      return fail(CHM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));             \
+  } while (0)
+
+struct LayerW {
+  const float *WAB, *Wcl, *b1, *D, *W2, *b2, *W3, *b3, *W4, *b4, *lw, *lb;
+};
+
+struct chm_model {
+  chm_dims d;
+  float* mem = nullptr;
+  size_t mem_floats = 0;
+  const float *emb, *Wc, *bc, *Wp, *bp, *fw, *fb, *Whead, *bhead, *Wlat, *flw, *flb;
+  std::vector<LayerW> layers;
+};
+
+struct chm_batch {
+  const chm_model* m;
+  int B, P;
+  long N, E;
+  std::vector<int> h_natoms;
+  // index tables
+  int *natoms, *node_off, *n2g, *ei, *ej;
+  long* edge_off;
+  // workspace
+  float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
+  std::vector<void*> allocs;
+  size_t bytes = 0;
+};
+
+extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
+extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.1 (gfx950, fp32 MFMA)"; }
+
+extern "C" int chm_num_params(const chm_dims* d) { return d ? 7 + 10 * d->num_layers + 6 : 0; }
+
+static int check_dims(const chm_dims* d) {
+  if (!d) return fail(CHM_E_ARG, "dims is NULL");
+  if (d->hidden_dim != H) return fail(CHM_E_UNSUPPORTED, "hidden_dim must be 512 in this build");
+  if (d->num_freqs != NF) return fail(CHM_E_UNSUPPORTED, "num_freqs must be 128 in this build");
+  if (d->time_dim != TD) return fail(CHM_E_UNSUPPORTED, "time_dim must be 128 in this build");
+  if (d->text_dim < 0 || (TD + d->text_dim) % 16) return fail(CHM_E_UNSUPPORTED, "time_dim + text_dim must be a multiple of 16");
+  if (d->max_atoms < 1 || d->max_atoms + 3 > HEADS_N) return fail(CHM_E_UNSUPPORTED, "max_atoms must be in [1, 125]");
+  if (d->num_layers < 1 || d->num_layers > 64) return fail(CHM_E_ARG, "num_layers out of range");
+  return CHM_OK;
+}
+
+extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int n_params, void* stream,
+                                chm_model** out) {
+  if (!out) return fail(CHM_E_ARG, "out is NULL");
+  *out = nullptr;
+  int rc = check_dims(dims);
+  if (rc) return rc;
+  if (n_params != chm_num_params(dims)) return fail(CHM_E_ARG, "wrong number of parameter tensors");
+  for (int i = 0; i < n_params; ++i)
+    if (!p[i]) return fail(CHM_E_ARG, "parameter pointer " + std::to_string(i) + " is NULL");
+  hipStream_t s = (hipStream_t)stream;
+  const int A = dims->max_atoms, L = dims->num_layers, X = dims->text_dim;
+  const int CIN = TD + X, W1K = 2 * H + 9 + FD;
+
+  // layout of the packed arena (each piece 256-byte aligned)
+  size_t off = 0;
+  auto take = [&](size_t n) { size_t o = off; off += (n + 63) / 64 * 64; return o; };
+  const size_t o_emb = take((size_t)A * H), o_Wc = take((size_t)2 * H * CIN), o_bc = take(2 * H), o_Wp = take(H * H),
+               o_bp = take(H), o_fw = take(H), o_fb = take(H);
+  std::vector<size_t> lo(L * 12);
+  for (int l = 0; l < L; ++l) {
+    lo[l * 12 + 0] = take((size_t)2 * H * H);  // WAB
+    lo[l * 12 + 1] = take((size_t)H * 9);      // Wcl
+    lo[l * 12 + 2] = take(H);                  // b1
+    lo[l * 12 + 3] = take((size_t)H * FD);     // D
+    lo[l * 12 + 4] = take((size_t)H * H);      // W2
+    lo[l * 12 + 5] = take(H);                  // b2
+    lo[l * 12 + 6] = take((size_t)H * 2 * H);  // W3
+    lo[l * 12 + 7] = take(H);                  // b3
+    lo[l * 12 + 8] = take((size_t)H * H);      // W4
+    lo[l * 12 + 9] = take(H);                  // b4
+    lo[l * 12 + 10] = take(H);                 // lw
+    lo[l * 12 + 11] = take(H);                 // lb
+  }
+  const size_t o_Wh = take((size_t)HEADS_N * H), o_bh = take(HEADS_N), o_Wl = take(9 * H), o_flw = take(H),
+               o_flb = take(H);
+
+  chm_model* m = new chm_model();
+  m->d = *dims;
+  m->mem_floats = off;
+  hipError_t e = hipMalloc(&m->mem, off * sizeof(float));
+  if (e != hipSuccess) {
+    delete m;
+    return fail(CHM_E_HIP, std::string("hipMalloc(model): ") + hipGetErrorString(e));
+  }
+  float* base = m->mem;
+  auto cp = [&](size_t o, const float* src, size_t n) {
+    return hipMemcpyAsync(base + o, src, n * sizeof(float), hipMemcpyDeviceToDevice, s);
+  };
+  // 2-D copy of a column block of a row-major [rows][src_ld] matrix
+  auto cp2 = [&](size_t o, size_t dst_ld, const float* src, size_t src_ld, size_t col0, size_t cols, size_t rows) {
+    return hipMemcpy2DAsync(base + o, dst_ld * sizeof(float), src + col0, src_ld * sizeof(float), cols * sizeof(float),
+                            rows, hipMemcpyDeviceToDevice, s);
+  };
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t _e = (x);                                                                       \
+    if (_e != hipSuccess) {                                                                    \
+      (void)hipFree(m->mem);                                                                   \
+      delete m;                                                                                \
+      return fail(CHM_E_HIP, std::string("weight packing: ") + hipGetErrorString(_e));         \
+    }                                                                                          \
+  } while (0)
+  CK(hipMemsetAsync(base, 0, off * sizeof(float), s));
+  CK(cp(o_emb, p[0], (size_t)A * H));
+  CK(cp(o_Wc, p[1], (size_t)2 * H * CIN));
+  CK(cp(o_bc, p[2], 2 * H));
+  CK(cp(o_Wp, p[3], H * H));
+  CK(cp(o_bp, p[4], H));
+  CK(cp(o_fw, p[5], H));
+  CK(cp(o_fb, p[6], H));
+  for (int l = 0; l < L; ++l) {
+    const float* const* q = p + 7 + 10 * l;
+    // edge_mlp.0.weight [H][2H+9+FD] -> WAB = [W1[:, 0:H] ; W1[:, H:2H]], Wcl = W1[:, 2H:2H+9], D = W1[:, 2H+9:]
+    CK(cp2(lo[l * 12 + 0], H, q[0], W1K, 0, H, H));
+    CK(cp2(lo[l * 12 + 0] + (size_t)H * H, H, q[0], W1K, H, H, H));
+    CK(cp2(lo[l * 12 + 1], 9, q[0], W1K, 2 * H, 9, H));
+    CK(cp2(lo[l * 12 + 3], FD, q[0], W1K, 2 * H + 9, FD, H));
+    CK(cp(lo[l * 12 + 2], q[1], H));
+    CK(cp(lo[l * 12 + 4], q[2], (size_t)H * H));
+    CK(cp(lo[l * 12 + 5], q[3], H));
+    CK(cp(lo[l * 12 + 6], q[4], (size_t)H * 2 * H));
+    CK(cp(lo[l * 12 + 7], q[5], H));
+    CK(cp(lo[l * 12 + 8], q[6], (size_t)H * H));
+    CK(cp(lo[l * 12 + 9], q[7], H));
+    CK(cp(lo[l * 12 + 10], q[8], H));
+    CK(cp(lo[l * 12 + 11], q[9], H));
+  }
+  const float* const* hq = p + 7 + 10 * L;  // coord_out.w, lattice_out.w, type_out.w, type_out.b, final_ln.w, final_ln.b
+  CK(cp(o_Wh, hq[2], (size_t)A * H));                 // rows 0..A-1: type_out
+  CK(cp(o_Wh + (size_t)A * H, hq[0], (size_t)3 * H)); // rows A..A+2: coord_out
+  CK(cp(o_bh, hq[3], A));
+  CK(cp(o_Wl, hq[1], 9 * H));
+  CK(cp(o_flw, hq[4], H));
+  CK(cp(o_flb, hq[5], H));
+  CK(hipStreamSynchronize(s));
+#undef CK
+  m->emb = base + o_emb; m->Wc = base + o_Wc; m->bc = base + o_bc; m->Wp = base + o_Wp; m->bp = base + o_bp;
+  m->fw = base + o_fw; m->fb = base + o_fb; m->Whead = base + o_Wh; m->bhead = base + o_bh; m->Wlat = base + o_Wl;
+  m->flw = base + o_flw; m->flb = base + o_flb;
+  m->layers.resize(L);
+  for (int l = 0; l < L; ++l) {
+    LayerW& w = m->layers[l];
+    const size_t* o = &lo[l * 12];
+    w.WAB = base + o[0]; w.Wcl = base + o[1]; w.b1 = base + o[2]; w.D = base + o[3]; w.W2 = base + o[4];
+    w.b2 = base + o[5]; w.W3 = base + o[6]; w.b3 = base + o[7]; w.W4 = base + o[8]; w.b4 = base + o[9];
+    w.lw = base + o[10]; w.lb = base + o[11];
+  }
+  *out = m;
+  return CHM_OK;
+}
+
+extern "C" void chm_model_destroy(chm_model* m) {
+  if (!m) return;
+  (void)hipFree(m->mem);
+  delete m;
+}
+
+extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, chm_batch** out) {
+  if (!out) return fail(CHM_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!m || !h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
+  if (max_pairs < 1 || max_pairs > 2) return fail(CHM_E_ARG, "max_pairs must be 1 or 2");
+  std::vector<int> nat(h_natoms, h_natoms + B), noff(B + 1), n2g;
+  std::vector<long> eoff(B + 1);
+  long N = 0, E = 0;
+  for (int g = 0; g < B; ++g) {
+    if (nat[g] < 1) return fail(CHM_E_ARG, "every crystal needs at least one atom");
+    noff[g] = (int)N;
+    eoff[g] = E;
+    N += nat[g];
+    E += (long)nat[g] * nat[g];
+  }
+  noff[B] = (int)N;
+  eoff[B] = E;
+  if (N > (1L << 30) || E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
+  n2g.resize(N);
+  std::vector<int> ei(E), ej(E);
+  for (int g = 0; g < B; ++g) {
+    for (int i = 0; i < nat[g]; ++i) n2g[noff[g] + i] = g;
+    long e = eoff[g];
+    for (int i = 0; i < nat[g]; ++i)
+      for (int j = 0; j < nat[g]; ++j, ++e) {
+        ei[e] = noff[g] + i;
+        ej[e] = noff[g] + j;
+      }
+  }
+  chm_batch* b = new chm_batch();
+  b->m = m;
+  b->B = B;
+  b->P = max_pairs;
+  b->N = N;
+  b->E = E;
+  b->h_natoms = nat;
+  const int P = max_pairs, L = m->d.num_layers, X = m->d.text_dim;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* ptr = nullptr;
+    if (hipMalloc(&ptr, bytes < 256 ? 256 : bytes) != hipSuccess) return nullptr;
+    b->allocs.push_back(ptr);
+    b->bytes += bytes;
+    return ptr;
+  };
+  bool ok = true;
+  auto fl = [&](size_t n) {
+    float* ptr = (float*)alloc(n * sizeof(float));
+    ok = ok && ptr;
+    return ptr;
+  };
+  b->natoms = (int*)alloc(B * sizeof(int));
+  b->node_off = (int*)alloc((B + 1) * sizeof(int));
+  b->edge_off = (long*)alloc((B + 1) * sizeof(long));
+  b->n2g = (int*)alloc(N * sizeof(int));
+  b->ei = (int*)alloc(E * sizeof(int));
+  b->ej = (int*)alloc(E * sizeof(int));
+  ok = b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej;
+  b->cin = fl((size_t)P * B * (TD + X));
+  b->cemb = fl((size_t)P * B * 2 * H);
+  b->Hres = fl((size_t)P * N * H);
+  b->Hl = fl((size_t)P * N * H);
+  b->Y = fl((size_t)P * N * H);
+  b->agg = fl((size_t)P * N * H);
+  b->PQ = fl((size_t)P * N * 2 * H);
+  b->gbias = fl((size_t)L * B * H);
+  b->F = fl((size_t)E * FD);
+  b->S = fl((size_t)P * E * H);
+  b->M = fl((size_t)P * E * H);
+  b->Hf = fl((size_t)P * N * H);
+  b->HO = fl((size_t)P * N * HEADS_N);
+  b->LAT = fl((size_t)P * B * 9);
+  if (!ok) {
+    chm_batch_destroy(b);
+    return fail(CHM_E_HIP, "hipMalloc failed for batch workspace");
+  }
+  hipError_t e = hipSuccess;
+  if (e == hipSuccess) e = hipMemcpy(b->natoms, nat.data(), B * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->node_off, noff.data(), (B + 1) * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->edge_off, eoff.data(), (B + 1) * sizeof(long), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->n2g, n2g.data(), N * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->ei, ei.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->ej, ej.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    chm_batch_destroy(b);
+    return fail(CHM_E_HIP, std::string("index upload: ") + hipGetErrorString(e));
+  }
+  *out = b;
+  return CHM_OK;
+}
+
+extern "C" void chm_batch_destroy(chm_batch* b) {
+  if (!b) return;
+  for (void* p : b->allocs) (void)hipFree(p);
+  delete b;
+}
+
+extern "C" size_t chm_batch_device_bytes(const chm_batch* b) { return b ? b->bytes : 0; }
+extern "C" int64_t chm_batch_num_nodes(const chm_batch* b) { return b ? b->N : -1; }
+extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -1; }
+
+static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const float* W, float* C, long ldc) {
+  GemmArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.A2 = A; g.lda2 = lda; g.ksplit = K;
+  g.W = W; g.ldw = K; g.C = C; g.ldc = ldc; g.gb_rowmod = 1;
+  return g;
+}
+
+// heads: bit 0 = node heads (types + coords), bit 1 = lattice head
+static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
+                       int tstride, const float* text0, const float* text1, int heads, hipStream_t s) {
+  const chm_model* m = b->m;
+  const int L = m->d.num_layers, X = m->d.text_dim, B = b->B;
+  const long N = b->N, E = b->E, R = (long)P * N;
+  const int CIN = TD + X;
+  HIPCHK(build_cond_in(temb, tstride, text0, text1, X, b->cin, B, P, s));
+  {
+    GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
+    g.bias = m->bc; g.act = 1;
+    HIPCHK(gemm(g, EPI_STD, s));
+  }
+  HIPCHK(embed(a, m->emb, b->Hres, N, P, s));
+  HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
+  for (int l = 0; l < L; ++l)
+    HIPCHK(graph_bias(lat, m->layers[l].Wcl, 9, m->layers[l].b1, b->gbias + (size_t)l * B * H, B, s));
+  for (int l = 0; l < L; ++l) {
+    const LayerW& w = m->layers[l];
+    {  // FiLM projection (cspnet.py:92)
+      GemmArgs g = gargs(R, H, H, b->Hres, H, m->Wp, b->Y, H);
+      g.bias = m->bp;
+      HIPCHK(gemm(g, EPI_STD, s));
+    }
+    HIPCHK(film_ln(b->Y, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s));
+    {  // per-node halves of the first edge layer: [P | Q] = Hl [A ; Bm]^T, P += b1 + C vec(LL^T)
+      GemmArgs g = gargs(R, 2 * H, H, b->Hl, H, w.WAB, b->PQ, 2 * H);
+      g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
+      HIPCHK(gemm(g, EPI_STD, s));
+    }
+    {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
+      GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
+      g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
+      HIPCHK(gemm(g, EPI_EDGE, s));
+    }
+    {  // edge layer 2: M = SiLU(S W2^T + b2)
+      GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
+      g.bias = w.b2; g.act = 1;
+      HIPCHK(gemm(g, EPI_STD, s));
+    }
+    HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
+    {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
+      GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);
+      g.A2 = b->agg; g.lda2 = H; g.ksplit = H; g.bias = w.b3; g.act = 1;
+      HIPCHK(gemm(g, EPI_STD, s));
+    }
+    {  // node MLP 2 + residual: Hres += SiLU(U W4^T + b4)
+      GemmArgs g = gargs(R, H, H, b->Y, H, w.W4, b->Hres, H);
+      g.bias = w.b4; g.act = 1; g.R = b->Hres; g.ldr = H;
+      HIPCHK(gemm(g, EPI_STD, s));
+    }
+  }
+  HIPCHK(layer_norm(b->Hres, b->Hf, R, m->flw, m->flb, s));
+  if (heads & 1) {
+    GemmArgs g = gargs(R, HEADS_N, H, b->Hf, H, m->Whead, b->HO, HEADS_N);
+    g.bias = m->bhead;
+    HIPCHK(gemm(g, EPI_STD, s));
+  }
+  if (heads & 2) HIPCHK(graph_heads(b->Hf, m->Wlat, lat, b->node_off, b->natoms, N, B, P, b->LAT, s));
+  return CHM_OK;
+}
+
+extern "C" int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* a, const float* x, const float* lat,
+                                   const float* temb, int time_stride, const float* text, float* types_out,
+                                   float* lattice_out, float* coords_out, float* node_out, void* stream) {
+  if (!b) return fail(CHM_E_ARG, "batch is NULL");
+  if (pairs < 1 || pairs > b->P) return fail(CHM_E_ARG, "pairs must be in [1, max_pairs]");
+  if (!a || !x || !lat || !temb) return fail(CHM_E_ARG, "inputs must not be NULL");
+  const int X = b->m->d.text_dim;
+  if (X > 0 && !text) return fail(CHM_E_ARG, "text embeddings required (text_dim > 0)");
+  hipStream_t s = (hipStream_t)stream;
+  const float* t0 = text;
+  const float* t1 = text ? text + (size_t)b->B * X : nullptr;
+  const int heads = ((types_out || coords_out) ? 1 : 0) | (lattice_out ? 2 : 0);
+  int rc = run_decoder(b, pairs, a, x, lat, temb, time_stride, t0, t1, heads, s);
+  if (rc) return rc;
+  const long R = (long)pairs * b->N;
+  if (heads & 1) HIPCHK(split_heads(b->HO, R, b->m->d.max_atoms, types_out, coords_out, s));
+  if (lattice_out)
+    HIPCHK(hipMemcpyAsync(lattice_out, b->LAT, (size_t)pairs * b->B * 9 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (node_out) HIPCHK(hipMemcpyAsync(node_out, b->Hf, (size_t)R * H * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return CHM_OK;
+}
+
+extern "C" int chm_sample_step(chm_batch* b, const chm_schedule* sc, int t, float cond_scale, int64_t* d_a, float* d_x,
+                               float* d_l, const float* d_cond, const float* d_null, const float* ra, const float* rl,
+                               const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
+                               int64_t graph_base, void* stream) {
+  if (!b || !sc) return fail(CHM_E_ARG, "batch / schedule is NULL");
+  if (b->P < 2) return fail(CHM_E_ARG, "sampling needs a batch created with max_pairs = 2");
+  if (t < 1 || t > sc->T) return fail(CHM_E_ARG, "t out of range");
+  if (!d_a || !d_x || !d_l || !sc->d_coef || !sc->d_time_emb || !sc->d_q_one_step || !sc->d_q_mats)
+    return fail(CHM_E_ARG, "NULL state or schedule table");
+  if (b->m->d.text_dim > 0 && (!d_cond || !d_null)) return fail(CHM_E_ARG, "cond / null embeddings required");
+  if (ra && !(rl && rx1 && rx2)) return fail(CHM_E_ARG, "host noise: all four tensors or none");
+  hipStream_t s = (hipStream_t)stream;
+  const float* temb = sc->d_time_emb + (size_t)t * TD;
+  int rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_cond, d_null, 3, s);
+  if (rc) return rc;
+  StepArgs sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.t = t; sa.T = sc->T; sa.A = b->m->d.max_atoms; sa.N = b->N; sa.B = b->B;
+  sa.cs_null = (float)(1.0 - (double)cond_scale); sa.cs_cond = cond_scale;
+  sa.coef = sc->d_coef; sa.q_one_step = sc->d_q_one_step; sa.q_mats = sc->d_q_mats;
+  sa.HO = b->HO; sa.LAT = b->LAT; sa.a = d_a; sa.x = d_x; sa.l = d_l; sa.n2g = b->n2g;
+  sa.ra = ra; sa.rl = rl; sa.rx1 = rx1; sa.rx2 = rx2;
+  sa.seed = seed; sa.node_base = node_base; sa.graph_base = graph_base;
+  HIPCHK(step_predictor(sa, s));
+  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_cond, d_null, 1, s);
+  if (rc) return rc;
+  HIPCHK(step_corrector(sa, s));
+  return CHM_OK;
+}
+
+extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, float* agg, void* stream) {
+  if (!b || !msg || !agg) return fail(CHM_E_ARG, "NULL argument");
+  if (pairs < 1) return fail(CHM_E_ARG, "pairs must be >= 1");
+  HIPCHK(segment_mean(msg, agg, b->n2g, b->node_off, b->edge_off, b->natoms, b->N, b->E, pairs, (hipStream_t)stream));
+  return CHM_OK;
+}
+
+extern "C" int chm_d3pm_sample(int N, int A, int T, const float* logits, const int64_t* xt, const int64_t* tn,
+                               const float* noise, const float* q1, const float* qm, int64_t* out, void* stream) {
+  if (N < 0 || A < 1 || A > 128 || T < 1) return fail(CHM_E_ARG, "bad sizes");
+  if (N == 0) return CHM_OK;
+  if (!logits || !xt || !tn || !noise || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
+  HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, noise, q1, qm, out, 0, 0, (hipStream_t)stream));
+  return CHM_OK;
+}
+
+extern "C" int chm_edge_features(chm_batch* b, const float* x, float* feat, void* stream) {
+  if (!b || !x || !feat) return fail(CHM_E_ARG, "NULL argument");
+  HIPCHK(fourier(x, b->ei, b->ej, b->E, feat, (hipStream_t)stream));
+  return CHM_OK;
+}

@@ -1,0 +1,295 @@
+"""Chemeleon sampler — drop-in for `chemeleon.modules.chemeleon.Chemeleon`
+on the sampling path (reference `chemeleon/modules/chemeleon.py:31-490`).
+
+Same constructor (`_config` dict of hyper-parameters), same buffers and
+state_dict keys (`beta_scheduler.*`, `sigma_scheduler.*`, `d3pm.*`,
+`decoder.*`), same `sample()` / `_sample_generator()` / `model_predictions()`
+signatures and return types. Each reverse step runs as one C-ABI call
+(`chm_sample_step`): the predictor and corrector classifier-free-guidance
+pairs, D3PM / DDPM / VE updates, all in HIP kernels on the caller's stream.
+
+Noise
+-----
+* ``noise="torch"`` (default, parity mode): every random tensor is drawn
+  from the global CPU torch generator in the reference's order
+  (chemeleon.py:348-349, 400-404, 418, 435, 455) and uploaded, so a run
+  seeded like the reference reproduces the reference CPU trajectory.
+* ``noise="philox"`` (throughput mode): noise is generated inside the step
+  kernels from a counter-based Philox stream keyed by (seed, t, global
+  node / graph index); results do not depend on how samples are sharded.
+
+Text conditioning is out of scope for the hot path (north star: "computed
+once on host and broadcast"): pass a `text_encoder` object with the
+reference's `get_text_embeds(texts, cond_drop_prob, device)` method, or pass
+`text_embeds=` / `null_text_embeds=` tensors directly.
+"""
+
+import os
+from typing import Any, Dict, Iterator, List, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from chemeleon_amd import _lib
+from chemeleon_amd.config import default_config
+from chemeleon_amd.modules.cspnet import CSPNet, SinusoidalTimeEmbeddings
+from chemeleon_amd.modules.schema import TrajectoryContainer, TrajectoryStep, step_to_atoms
+from chemeleon_amd.utils.diff_utils import D3PM, BetaScheduler, SigmaScheduler
+
+CHECKPOINT_DIR = os.environ.get("CHEMELEON_CHECKPOINT_DIR",
+                                os.path.join(os.path.dirname(os.path.dirname(__file__)), "checkpoints"))
+# file names of the released checkpoints (reference chemeleon/constants.py:3-7)
+PATH_CHEMELEON_GENERAL_TEXT = os.path.join(CHECKPOINT_DIR, "chemeleon-7fsg68c3.ckpt")
+PATH_CHEMELEON_COMPOSITION = os.path.join(CHECKPOINT_DIR, "chemeleon-fksq6cgp.ckpt")
+
+
+class Chemeleon(nn.Module):
+    def __init__(self, _config: Dict[str, Any], text_encoder=None, **kwargs):
+        super().__init__()
+        cfg = default_config()
+        cfg.update(_config)
+        self.hparams = cfg
+        self.time_embed = SinusoidalTimeEmbeddings(cfg["time_dim"])
+        self.text_guide = cfg["text_guide"]
+        self.cond_drop_prob = cfg.get("cond_drop_prob", 0.2)
+        self.text_encoder = text_encoder
+        self.num_timesteps = cfg["timesteps"]
+        self.beta_scheduler = BetaScheduler(timesteps=self.num_timesteps, scheduler_mode=cfg["beta_schedule"])
+        self.sigma_scheduler = SigmaScheduler(timesteps=self.num_timesteps)
+        self.max_atoms = cfg["max_atoms"]
+        self.d3pm = D3PM(beta_scheduler=self.beta_scheduler, num_timesteps=cfg["timesteps"],
+                         max_atoms=cfg["max_atoms"], d3pm_hybrid_coeff=cfg["d3pm_hybrid_coeff"])
+        self.mask_lattice_matrix = torch.tensor([[1, 0, 1], [1, 1, 1], [0, 0, 1]]).bool()  # chemeleon.py:70-72
+        self.decoder = CSPNet(hidden_dim=cfg["hidden_dim"], time_dim=cfg["time_dim"],
+                              text_dim=cfg["text_dim"] if self.text_guide else 0, num_layers=cfg["num_layers"],
+                              max_atoms=cfg["max_atoms"], act_fn=cfg["act_fn"], dis_emb=cfg["dis_emb"],
+                              num_freqs=cfg["num_freqs"], edge_style=cfg["edge_style"], cutoff=cfg["cutoff"],
+                              max_neighbors=cfg["max_neighbors"], ln=cfg["ln"], ip=cfg["ip"], smooth=cfg["smooth"],
+                              pred_atom_types=cfg["pred_atom_types"])
+        self._tables: Dict[Tuple, Tuple] = {}
+
+    # ------------------------------------------------------------------ loading
+    @property
+    def device(self):
+        return next(self.decoder.parameters()).device
+
+    @classmethod
+    def load_from_checkpoint(cls, path: str, text_encoder=None, map_location="cpu", strict: bool = True, **kwargs):
+        """Lightning checkpoint -> model (reference chemeleon.py:113-115 via
+        LightningModule.load_from_checkpoint). Loaded with weights_only=True.
+        Buffers (schedules, sigmas_norm, D3PM tables) come from the file."""
+        ck = torch.load(path, map_location=map_location, weights_only=True)
+        hp = dict(ck.get("hyper_parameters", {}))
+        hp.update(kwargs)
+        m = cls(hp, text_encoder=text_encoder)
+        sd = ck["state_dict"]
+        own = {k: v for k, v in sd.items() if not k.startswith("text_encoder.")}
+        missing, unexpected = m.load_state_dict(own, strict=False)
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"checkpoint mismatch: missing {missing}, unexpected {unexpected}")
+        if text_encoder is not None and isinstance(text_encoder, nn.Module):
+            te = {k[len("text_encoder."):]: v for k, v in sd.items() if k.startswith("text_encoder.")}
+            if te:
+                text_encoder.load_state_dict(te, strict=False)
+        return m
+
+    @classmethod
+    def _load_released(cls, path, **kwargs):
+        if not os.path.exists(path):
+            raise FileNotFoundError(
+                f"{path} not found. The released checkpoints are downloaded by the reference from figshare "
+                "(chemeleon/constants.py:9-14); this build does not download. Place the file there or set "
+                "CHEMELEON_CHECKPOINT_DIR.")
+        return cls.load_from_checkpoint(path, **kwargs)
+
+    @classmethod
+    def load_general_text_model(cls, *args, **kwargs):
+        return cls._load_released(PATH_CHEMELEON_GENERAL_TEXT, **kwargs)
+
+    @classmethod
+    def load_composition_model(cls, *args, **kwargs):
+        return cls._load_released(PATH_CHEMELEON_COMPOSITION, **kwargs)
+
+    # ------------------------------------------------------------------ tables
+    def schedule_tables(self, step_lr: float):
+        """Per-t scalar coefficients computed with the reference's own fp32
+        expressions (chemeleon.py:413-457) on the host, once; plus the
+        time-embedding table (cspnet.py:28-35). Returns (chm_schedule, keepalive)."""
+        dev = self.device
+        key = (str(dev), float(step_lr))
+        if key in self._tables:
+            return self._tables[key]
+        T = self.num_timesteps
+        bs, ss = self.beta_scheduler, self.sigma_scheduler
+        al_, ac_, sg_ = bs.alphas.cpu(), bs.alphas_cumprod.cpu(), bs.sigmas.cpu()
+        sx_, sn_ = ss.sigmas.cpu(), ss.sigmas_norm.cpu()
+        coef = torch.zeros(T + 1, 8)
+        for t in range(1, T + 1):
+            alphas, alphas_cumprod, sigmas = al_[t], ac_[t], sg_[t]
+            c0 = 1.0 / torch.sqrt(alphas)
+            c1 = (1 - alphas) / torch.sqrt(1 - alphas_cumprod)
+            sigma_x, sigma_norm, adj = sx_[t], sn_[t], sx_[t - 1]
+            step_size = sigma_x ** 2 - adj ** 2
+            std_x = torch.sqrt((adj ** 2 * (sigma_x ** 2 - adj ** 2)) / (sigma_x ** 2))
+            step2 = step_lr * (sigma_x / ss.sigma_begin) ** 2
+            std2 = torch.sqrt(2 * step2)
+            coef[t] = torch.stack([c0, c1, sigmas, step_size, std_x, torch.sqrt(sigma_norm), step2, std2])
+        temb = self.time_embed(torch.arange(T + 1))
+        coef_d = coef.to(dev).contiguous()
+        temb_d = temb.float().to(dev).contiguous()
+        q1 = self.d3pm.q_one_step_mats.to(dev).float().contiguous()
+        qm = self.d3pm.q_mats.to(dev).float().contiguous()
+        sched = _lib.chm_schedule(T, coef_d.data_ptr(), temb_d.data_ptr(), q1.data_ptr(), qm.data_ptr())
+        self._tables[key] = (sched, (coef_d, temb_d, q1, qm))
+        return self._tables[key]
+
+    # ------------------------------------------------------------------ API
+    def model_predictions(self, time_emb, atom_types, frac_coords, lattices, batch_natoms, batch_idx,
+                          cond_scale: float, text_embeds=None, null_text_embeds=None):
+        """chemeleon.py:246-303 (both CFG decoder calls run as one batched
+        HIP call)."""
+        if self.text_guide:
+            types, lat, coords, _ = self.decoder.forward_cfg(atom_types, frac_coords, lattices, batch_natoms,
+                                                             time_emb, text_embeds, null_text_embeds)
+            mix = lambda p: (1 - cond_scale) * p[1] + cond_scale * p[0]  # noqa: E731
+            return mix(types), mix(lat), mix(coords)
+        out = self.decoder(t=time_emb, atom_types=atom_types, frac_coords=frac_coords, lattices=lattices,
+                           num_atoms=batch_natoms, node2graph=batch_idx)
+        return out.atom_types_out, out.lattice_out, out.coords_out
+
+    def _conditioning(self, texts, B, text_embeds, null_text_embeds):
+        dev = self.device
+        if not self.text_guide:
+            return None, None
+        if text_embeds is None or null_text_embeds is None:
+            if self.text_encoder is None:
+                raise RuntimeError("text_guide model: pass text_encoder=... or text_embeds=/null_text_embeds=")
+            if texts is None:
+                raise ValueError("texts are required for a text-guided model")
+            text_embeds = self.text_encoder.get_text_embeds(texts, cond_drop_prob=0.0, device=dev)
+            null_text_embeds = self.text_encoder.get_text_embeds(texts, cond_drop_prob=1.0, device=dev)
+        cond = text_embeds.float().to(dev).expand(B, -1).contiguous()
+        null = null_text_embeds.float().to(dev).expand(B, -1).contiguous()
+        return cond, null
+
+    @torch.no_grad()
+    def sample_states(self, natoms: Union[int, List[int]], texts: Optional[Union[str, List[str]]] = None,
+                      cond_scale: float = 2.0, step_lr: float = 1e-5, *, noise: str = "torch", seed: int = 0,
+                      text_embeds=None, null_text_embeds=None, clone: bool = True, t_stop: int = 0,
+                      node_base: int = 0, graph_base: int = 0,
+                      init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Iterator[Tuple]:
+        """Reverse loop of chemeleon.py:305-467 yielding device tensors
+        (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
+        starting with the pure-noise state at t = T."""
+        if isinstance(natoms, int):
+            natoms = [natoms]
+        natoms = [int(n) for n in natoms]
+        if texts is not None and isinstance(texts, str):
+            texts = [texts]
+        if texts is not None and len(texts) != len(natoms):
+            raise ValueError("natoms and texts must have the same number of elements.")
+        if noise not in ("torch", "philox"):
+            raise ValueError("noise must be 'torch' or 'philox'")
+        dev = self.device
+        if dev.type != "cuda":
+            raise RuntimeError("Chemeleon (chemeleon_amd) samples on a HIP device only; call .to('cuda') first")
+        B, N, A, T = len(natoms), sum(natoms), self.max_atoms, self.num_timesteps
+        mask = self.mask_lattice_matrix
+        a = torch.zeros(N, dtype=torch.long, device=dev)  # chemeleon.py:347 (absorbing class 0)
+        if init is not None:
+            l0, x0 = init
+        elif noise == "torch":
+            l0 = torch.randn(B, 3, 3) * mask  # :348
+            x0 = torch.randn(N, 3)  # :349
+        else:
+            g = torch.Generator().manual_seed(seed)
+            l0 = torch.randn(B, 3, 3, generator=g) * mask
+            x0 = torch.randn(N, 3, generator=g)
+        lat = l0.float().to(dev).contiguous()
+        x = (x0 % 1.0).float().to(dev).contiguous()  # :359
+        cond, null = self._conditioning(texts, B, text_embeds, null_text_embeds)
+        if not self.text_guide:
+            cond_scale = 1.0  # one conditioning: the CFG mix degenerates to the plain prediction
+        sched, _keep = self.schedule_tables(step_lr)
+        batch = self.decoder.hip_batch(natoms, max_pairs=2)
+        L = _lib.load()
+        stream = _lib.stream_handle(dev)
+        emit = (lambda *ts: tuple(t.clone() for t in ts)) if clone else (lambda *ts: ts)
+        yield (T,) + emit(a, x, lat)
+        for t in range(T, t_stop, -1):
+            if noise == "torch" and t > 1:
+                ra = torch.rand((N, A)).to(dev, non_blocking=False)  # :400-404
+                rl = torch.randn(B, 3, 3).to(dev)  # :418
+                rx1 = torch.randn(N, 3).to(dev)  # :435
+                rx2 = torch.randn(N, 3).to(dev)  # :455
+                nz = (ra, rl, rx1, rx2)
+            else:
+                nz = (None, None, None, None)
+            _lib.check(L.chm_sample_step(batch.handle, sched, t, float(cond_scale), _lib.ptr(a), _lib.ptr(x),
+                                         _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null), *[_lib.ptr(z) for z in nz],
+                                         seed, node_base, graph_base, stream), "chm_sample_step")
+            yield (t - 1,) + emit(a, x, lat)
+
+    @torch.no_grad()
+    def reverse_step(self, t: int, atom_types, frac_coords, lattices, natoms: List[int], cond_scale: float = 2.0,
+                     step_lr: float = 1e-5, text_embeds=None, null_text_embeds=None, noise=None, seed: int = 0):
+        """One step t -> t-1 (chemeleon.py:379-466) from an explicit state.
+        `noise` = (rand_a, rand_l, rand_x1, rand_x2) tensors or None (Philox).
+        Returns new (atom_types, frac_coords, lattices) device tensors."""
+        dev = self.device
+        natoms = [int(n) for n in natoms]
+        a = atom_types.to(dev).long().clone().contiguous()
+        x = frac_coords.to(dev).float().clone().contiguous()
+        lat = lattices.to(dev).float().clone().contiguous()
+        cond, null = self._conditioning(None, len(natoms), text_embeds, null_text_embeds)
+        if not self.text_guide:
+            cond_scale = 1.0
+        sched, _keep = self.schedule_tables(step_lr)
+        batch = self.decoder.hip_batch(natoms, max_pairs=2)
+        nz = [None] * 4 if noise is None else [z.to(dev).float().contiguous() for z in noise]
+        _lib.require_device(a, x, lat, cond, null, *nz)
+        _lib.check(_lib.load().chm_sample_step(batch.handle, sched, int(t), float(cond_scale), _lib.ptr(a),
+                                               _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null),
+                                               *[_lib.ptr(z) for z in nz], seed, 0, 0, _lib.stream_handle(dev)),
+                   "chm_sample_step")
+        return a, x, lat
+
+    @torch.no_grad()
+    def _sample_generator(self, natoms: Union[int, List[int]], texts: Optional[Union[str, List[str]]] = None,
+                          cond_scale: float = 2.0, step_lr: float = 1e-5, **kw):
+        """chemeleon.py:305-467: yields, for every step t -> t-1, the list of
+        structures at t-1 (TrajectoryContainer.get_atoms, schema.py:57-83)."""
+        if isinstance(natoms, int):
+            natoms = [natoms]
+        it = self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw)
+        next(it)
+        for t, a, x, lat in it:
+            yield step_to_atoms(a, x, lat, natoms)
+
+    def sample(self, text_input: str, n_atoms: int, n_samples: int, cond_scale: float = 2.0, step_lr: float = 1e-5,
+               return_trajectory: bool = False, stream: bool = False, **kw):
+        """chemeleon.py:469-490. Without return_trajectory / stream, only the
+        final state is copied to the host (the reference converts every step)."""
+        natoms = [n_atoms] * n_samples
+        texts = [text_input] * n_samples if text_input is not None else None
+        if stream:
+            return self._sample_generator(natoms, texts, cond_scale, step_lr, **kw)
+        if return_trajectory:
+            return list(self._sample_generator(natoms, texts, cond_scale, step_lr, **kw))
+        last = None
+        for last in self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw):
+            pass
+        _, a, x, lat = last
+        return step_to_atoms(a, x, lat, natoms)
+
+    def trajectory_container(self, natoms, texts=None, cond_scale=2.0, step_lr=1e-5, **kw) -> TrajectoryContainer:
+        """All states t = T..0 as the reference's TrajectoryContainer."""
+        if isinstance(natoms, int):
+            natoms = [natoms]
+        tc = TrajectoryContainer(total_steps=self.num_timesteps)
+        nat = torch.tensor(natoms)
+        bidx = torch.arange(len(natoms)).repeat_interleave(nat)
+        for t, a, x, lat in self.sample_states(natoms, texts, cond_scale, step_lr, clone=True, **kw):
+            tc[t] = TrajectoryStep(num_atoms=nat, atom_types=a.cpu(), frac_coords=x.cpu(), lattices=lat.cpu(),
+                                   batch_idx=bidx)
+        return tc

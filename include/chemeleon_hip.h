@@ -1,0 +1,163 @@
+/* chemeleon_hip.h — C ABI of the MI355X (gfx950) sampling path of Chemeleon.
+ *
+ * The hot path of ryannduma/chemeleon is the reverse-diffusion loop
+ * `Chemeleon.sample()` -> `_sample_generator()` -> `model_predictions()` ->
+ * `CSPNet.forward()` plus the D3PM / DDPM / VE predictor-corrector updates
+ * (chemeleon/modules/chemeleon.py:246-490, chemeleon/modules/cspnet.py:184-405,
+ * chemeleon/utils/diff_utils.py:152-329). The reference is pure Python over
+ * ATen, so there is no reference C interface to replace; each entry point
+ * below names the Python interface whose behaviour it takes over.
+ *
+ * Conventions
+ *  - Every pointer argument named d_* is a DEVICE pointer, caller-owned,
+ *    fp32 unless stated; int64 where the reference uses torch.long.
+ *  - All work is enqueued on the caller's HIP stream `stream`
+ *    (a hipStream_t passed as void*); nothing synchronises the host except
+ *    chm_model_create / chm_batch_create (setup).
+ *  - No allocation inside chm_decoder_forward / chm_sample_step: the batch
+ *    object owns a workspace sized at creation. Calls are graph-capturable.
+ *  - Every function returns 0 on success or a negative CHM_E_* code;
+ *    chm_last_error() returns a thread-local message for the last failure.
+ *  - Conditioning index c: 0 = text ("cond"), 1 = null text ("null").
+ */
+#ifndef CHEMELEON_HIP_H
+#define CHEMELEON_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHM_OK 0
+#define CHM_E_ARG (-1)      /* bad argument / shape */
+#define CHM_E_HIP (-2)      /* HIP runtime error */
+#define CHM_E_UNSUPPORTED (-3)
+
+/* Hyper-parameters of the score network; mirrors the CSPNet constructor
+ * (chemeleon/modules/cspnet.py:185-202). This build implements
+ * hidden_dim = 512, num_freqs = 128, edge_style "fc", ln = ip = 1,
+ * smooth = 0, act "silu", dis_emb "sin"; other values return
+ * CHM_E_UNSUPPORTED from chm_model_create. */
+typedef struct {
+  int hidden_dim;  /* 512 */
+  int time_dim;    /* 128 */
+  int text_dim;    /* 512 */
+  int num_layers;  /* 6 */
+  int max_atoms;   /* 104 classes (103 elements + dummy) */
+  int num_freqs;   /* 128 */
+} chm_dims;
+
+typedef struct chm_model chm_model;
+typedef struct chm_batch chm_batch;
+
+/* Last error message of the calling thread ("" if none). */
+const char* chm_last_error(void);
+
+/* Version string of the library build. */
+const char* chm_version(void);
+
+/* Number of decoder parameter tensors chm_model_create expects for `dims`
+ * (= len(CSPNet.state_dict()) for ln=True, smooth=False). */
+int chm_num_params(const chm_dims* dims);
+
+/* Builds the packed device copy of the decoder weights.
+ * Replaces: CSPNet.__init__ + load_state_dict (cspnet.py:185-234).
+ * d_params[i] points to the i-th state_dict tensor in this order (row-major,
+ * contiguous, fp32, nn.Linear layout [out][in]):
+ *   node_embedding.weight, film_layer.mlp_cond.0.{weight,bias},
+ *   film_layer.proj.{weight,bias}, film_layer.norm.{weight,bias},
+ *   for l in 0..L-1: csp_layer_l.{edge_mlp.0.weight, edge_mlp.0.bias,
+ *     edge_mlp.2.weight, edge_mlp.2.bias, node_mlp.0.weight, node_mlp.0.bias,
+ *     node_mlp.2.weight, node_mlp.2.bias, layer_norm.weight, layer_norm.bias},
+ *   coord_out.weight, lattice_out.weight, type_out.{weight,bias},
+ *   final_layer_norm.{weight,bias}.
+ * Synchronises `stream` before returning. */
+int chm_model_create(const chm_dims* dims, const float* const* d_params, int n_params, void* stream,
+                     chm_model** out);
+void chm_model_destroy(chm_model* m);
+
+/* Describes a (possibly ragged) batch of crystals and owns the workspace of
+ * its decoder calls. Replaces: Batch.from_data_list + the fc edge builder
+ * (chemeleon.py:335-343, cspnet.py:319-324): node i of crystal g is global
+ * node node_off[g] + i; the fully connected edges of crystal g are visited in
+ * the reference's row-major (i, j) order, self loops included, but never
+ * materialised as a dense N x N matrix. `max_pairs` is 1 (plain decoder
+ * calls) or 2 (cond + null classifier-free-guidance pairs). */
+int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs, chm_batch** out);
+void chm_batch_destroy(chm_batch* b);
+/* Device bytes the batch allocated (workspace + index tables). */
+size_t chm_batch_device_bytes(const chm_batch* b);
+
+/* One decoder call for `pairs` conditionings that share atom types,
+ * coordinates and lattices (pairs = 1: CSPNet.forward, cspnet.py:345-405;
+ * pairs = 2: the two calls of Chemeleon.model_predictions, chemeleon.py:258-285).
+ *   d_atom_types [N] int64, d_frac [N,3], d_lattices [B,3,3]
+ *   d_time_emb   [B,128] rows, row stride time_stride floats (0 = one row for all graphs)
+ *   d_text       [pairs,B,text_dim] (row stride text_dim) or NULL if text_dim == 0
+ * Outputs (any may be NULL to skip it):
+ *   d_types_out [pairs,N,A], d_lattice_out [pairs,B,3,3], d_coords_out [pairs,N,3],
+ *   d_node_out  [pairs,N,H] (final-LayerNorm node features). */
+int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* d_atom_types, const float* d_frac,
+                        const float* d_lattices, const float* d_time_emb, int time_stride, const float* d_text,
+                        float* d_types_out, float* d_lattice_out, float* d_coords_out, float* d_node_out,
+                        void* stream);
+
+/* Per-timestep schedule tables (device, fp32), computed once by the host from
+ * the reference schedules (diff_utils.py:57-131, chemeleon.py:413-457):
+ *   d_coef [T+1][8]: {c0, c1, sigma_l, step_x, std_x, sqrt(sigma_norm),
+ *                     step_lr*(sigma_t/sigma_begin)^2, sqrt(2*that)}
+ *   d_time_emb [T+1][time_dim]: SinusoidalTimeEmbeddings(t) (cspnet.py:21-35)
+ *   d_q_one_step, d_q_mats [T+1][A][A]: D3PM buffers (diff_utils.py:168-185) */
+typedef struct {
+  int T;
+  const float* d_coef;
+  const float* d_time_emb;
+  const float* d_q_one_step;
+  const float* d_q_mats;
+} chm_schedule;
+
+/* One reverse-diffusion step t -> t-1 of Chemeleon._sample_generator
+ * (chemeleon.py:379-466): predictor CFG pair, D3PM atom-type sampling
+ * (diff_utils.py:307-329), DDPM lattice update (clip at t == T), VE
+ * predictor half step, corrector CFG pair, Langevin corrector, wrap to [0,1).
+ * State is updated in place: d_a [N] int64, d_x [N,3], d_l [B,3,3].
+ * d_cond, d_null: [B,text_dim] conditioning vectors.
+ * Noise: if d_rand_a != NULL the four host-drawn tensors of the reference's
+ * RNG stream are used (parity mode): rand_a [N,A] uniform, rand_l [B,3,3],
+ * rand_x1 [N,3], rand_x2 [N,3] normals; they are ignored at t == 1 as in the
+ * reference. If d_rand_a == NULL, noise comes from a counter-based Philox
+ * generator keyed by (seed, t, global node / graph index), so results do not
+ * depend on how samples are sharded across GPUs. `node_base`/`graph_base`
+ * are the global indices of this batch's first node / graph for that key. */
+int chm_sample_step(chm_batch* b, const chm_schedule* sched, int t, float cond_scale, int64_t* d_a, float* d_x,
+                    float* d_l, const float* d_cond, const float* d_null, const float* d_rand_a,
+                    const float* d_rand_l, const float* d_rand_x1, const float* d_rand_x2, uint64_t seed,
+                    int64_t node_base, int64_t graph_base, void* stream);
+
+/* Standalone message-passing aggregation (scatter_mean of edge messages onto
+ * their source node; chemeleon/utils/scatter.py:88-112 as called from
+ * cspnet.py:155-160) over this batch's fc edge layout:
+ *   d_msg [pairs,E,H] -> d_agg [pairs,N,H], agg[i] = sum_j msg[(i,j)] / max(n_g,1). */
+int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, float* d_agg, void* stream);
+
+/* D3PM reverse sampling for explicit inputs (diff_utils.py:307-329):
+ * d_logits [N,A], d_xt [N] int64, d_t [N] int64 per-node timestep,
+ * d_noise [N,A] uniform -> d_out [N] int64. Tables as in chm_schedule. */
+int chm_d3pm_sample(int N, int A, int T, const float* d_logits, const int64_t* d_xt, const int64_t* d_t,
+                    const float* d_noise, const float* d_q_one_step, const float* d_q_mats, int64_t* d_out,
+                    void* stream);
+
+/* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
+ * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */
+int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* stream);
+
+/* Sizes of the batch (for callers that allocate outputs). */
+int64_t chm_batch_num_nodes(const chm_batch* b);
+int64_t chm_batch_num_edges(const chm_batch* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHEMELEON_HIP_H */

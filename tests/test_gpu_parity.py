@@ -1,0 +1,216 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and with the
+reference-generated golden fixtures. Run on an MI355X: pytest -m gpu.
+
+Tolerances (north star: 1e-4 relative fp32, atom types bit-exact):
+* decoder outputs: |gpu - ref| <= 1e-4 * max(|ref|, 1) elementwise-scaled
+  (rtol 1e-4 with an absolute floor of 1e-4 times the tensor's RMS scale);
+* atom types: bit-exact;
+* fractional coordinates: periodic distance min(|d|, 1 - |d|) <= 1e-4;
+* lattices: rtol 1e-4 (absolute floor 1e-4 x max |lattice|).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from chemeleon_amd import _lib
+from chemeleon_amd.config import default_config
+from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds, weights_crc
+from oracle import chemeleon_oracle as O
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a HIP device")]
+
+DEV = "cuda"
+
+
+def close(gpu, ref, rtol=1e-4, what=""):
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    scale = max(np.sqrt(np.mean(ref ** 2)), 1e-12)
+    err = np.abs(gpu - ref) / np.maximum(np.abs(ref), scale)
+    assert np.isfinite(gpu).all(), f"{what}: non-finite output"
+    assert err.max() <= rtol, f"{what}: max scaled error {err.max():.3e} > {rtol}"
+    return err.max()
+
+
+def periodic_close(gpu, ref, tol=1e-4, what=""):
+    d = np.abs(np.asarray(gpu, np.float64) - np.asarray(ref, np.float64))
+    d = np.minimum(d, 1.0 - d)
+    assert d.max() <= tol, f"{what}: max periodic error {d.max():.3e}"
+    return d.max()
+
+
+def _model(T):
+    from chemeleon_amd import Chemeleon
+    cfg = default_config()
+    cfg["timesteps"] = T
+    torch.manual_seed(0)  # sigmas_norm Monte-Carlo draws, as when the fixtures were made
+    m = Chemeleon(cfg)
+    m.decoder.load_state_dict(synthetic_state_dict(default_config()))
+    return m.to(DEV).eval()
+
+
+@pytest.fixture(scope="module")
+def model1000():
+    return _model(1000)
+
+
+@pytest.fixture(scope="module")
+def model100():
+    return _model(100)
+
+
+@pytest.fixture(scope="module")
+def cn():
+    c, n = synthetic_text_embeds(512)
+    return c, n
+
+
+# --------------------------------------------------------------------------- kernels
+def test_fourier_features(model1000, golden):
+    g = golden("decoder_ragged.npz")
+    nat = g["natoms"].tolist()
+    x = torch.from_numpy(g["frac"])
+    b = model1000.decoder.hip_batch(nat, 1)
+    feat = torch.empty(b.num_edges, 768, device=DEV)
+    xd = x.to(DEV)
+    _lib.check(_lib.load().chm_edge_features(b.handle, _lib.ptr(xd), _lib.ptr(feat), _lib.stream_handle()), "fe")
+    e = O.fc_edges(nat)
+    ref = O.fourier((x[e[1]] - x[e[0]]) % 1.0, 128)
+    np.testing.assert_allclose(feat.cpu().numpy(), ref.numpy(), atol=2e-6, rtol=0)
+
+
+def test_segment_mean_matches_oracle(model1000):
+    nat = [3, 7, 1, 12, 40]
+    b = model1000.decoder.hip_batch(nat, 2)
+    gen = torch.Generator().manual_seed(3)
+    msg = torch.randn(2, b.num_edges, 512, generator=gen)
+    agg = torch.empty(2, b.num_nodes, 512, device=DEV)
+    md = msg.to(DEV)
+    _lib.check(_lib.load().chm_segment_mean(b.handle, 2, _lib.ptr(md), _lib.ptr(agg), _lib.stream_handle()), "sm")
+    e = O.fc_edges(nat)
+    for c in range(2):
+        ref = O.scatter_mean(msg[c], e[0], b.num_nodes)
+        np.testing.assert_allclose(agg[c].cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_d3pm_bit_exact(model100, golden):
+    g = golden("units.npz")
+    dp = model100.d3pm
+    out = dp.p_logits(torch.from_numpy(g["d3pm_logits"]).to(DEV), torch.from_numpy(g["d3pm_xt"]).to(DEV),
+                      torch.from_numpy(g["d3pm_t"]).to(DEV), torch.from_numpy(g["d3pm_u"]).to(DEV))
+    np.testing.assert_array_equal(out.cpu().numpy(), g["d3pm_out"])
+
+
+# --------------------------------------------------------------------------- decoder
+@pytest.mark.parametrize("name", ["decoder_4x6.npz", "decoder_ragged.npz"])
+def test_decoder_forward(model1000, golden, name, cn):
+    g = golden(name)
+    sd = model1000.decoder.state_dict()
+    assert weights_crc({k: v.cpu() for k, v in sd.items()}) == int(g["weights_crc"])
+    nat = torch.from_numpy(g["natoms"])
+    B = len(nat)
+    te = model1000.time_embed(torch.full((B,), int(g["t"]), dtype=torch.long)).to(DEV)
+    out = model1000.decoder(atom_types=torch.from_numpy(g["atom_types"]).to(DEV),
+                            frac_coords=torch.from_numpy(g["frac"]).to(DEV),
+                            lattices=torch.from_numpy(g["lattices"]).to(DEV), num_atoms=nat.to(DEV),
+                            node2graph=torch.arange(B).repeat_interleave(nat).to(DEV), t=te,
+                            text_embeds=cn[0].expand(B, -1).to(DEV))
+    close(out.node_features.cpu(), g["node_features"], what="node_features")
+    close(out.atom_types_out.cpu(), g["types"], what="types")
+    close(out.coords_out.cpu(), g["coords"], what="coords")
+    close(out.lattice_out.cpu(), g["lattice_out"], what="lattice")
+
+
+def test_cfg_pair(model1000, golden, cn):
+    g = golden("decoder_4x6.npz")
+    nat = torch.from_numpy(g["natoms"])
+    B = len(nat)
+    te = model1000.time_embed(torch.full((B,), int(g["t"]), dtype=torch.long)).to(DEV)
+    pa, pl, px = model1000.model_predictions(te, torch.from_numpy(g["atom_types"]).to(DEV),
+                                             torch.from_numpy(g["frac"]).to(DEV),
+                                             torch.from_numpy(g["lattices"]).to(DEV), nat.to(DEV), None, 2.0,
+                                             cn[0].expand(B, -1).to(DEV), cn[1].expand(B, -1).to(DEV))
+    close(pa.cpu(), g["cfg_types"], what="cfg types")
+    close(pl.cpu(), g["cfg_lattice"], what="cfg lattice")
+    close(px.cpu(), g["cfg_coords"], what="cfg coords")
+
+
+# --------------------------------------------------------------------------- sampler
+@pytest.mark.parametrize("tag", ["64x20", "16x40"])
+def test_teacher_forced_steps(model1000, golden, cn, tag):
+    """Reference state at t + the reference's noise stream -> state at t-1."""
+    g = golden(f"step_{tag}.npz")
+    nat = g["natoms"].tolist()
+    B, N = len(nat), sum(nat)
+    for t in g["ts"]:
+        t = int(t)
+        torch.manual_seed(5000 + t)
+        nz = None
+        if t > 1:
+            nz = (torch.rand((N, 104)), torch.randn(B, 3, 3), torch.randn(N, 3), torch.randn(N, 3))
+        a, x, lat = model1000.reverse_step(t, torch.from_numpy(g[f"t{t}_a"]), torch.from_numpy(g[f"t{t}_x"]),
+                                           torch.from_numpy(g[f"t{t}_l"]), nat, 2.0, 1e-5, cn[0], cn[1],
+                                           noise=nz if nz is not None else None)
+        np.testing.assert_array_equal(a.cpu().numpy(), g[f"t{t}_a_out"], err_msg=f"atom types t={t}")
+        periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"frac t={t}")
+        close(lat.cpu(), g[f"t{t}_l_out"], what=f"lattice t={t}")
+
+
+def test_trajectory_c0(model100, golden, cn):
+    """C0 (configs[0]): 4 x 6 atoms, T = 100, seed 42, the full sampler."""
+    g = golden("trajectory_4x6_T100.npz")
+    torch.manual_seed(42)
+    states = list(model100.sample_states([6] * 4, None, 2.0, 1e-5, noise="torch", text_embeds=cn[0],
+                                         null_text_embeds=cn[1]))[1:]
+    a = np.stack([s[1].cpu().numpy() for s in states])
+    x = np.stack([s[2].cpu().numpy() for s in states])
+    lat = np.stack([s[3].cpu().numpy() for s in states])
+    np.testing.assert_array_equal(a, g["atom_types"])
+    periodic_close(x, g["frac"], what="trajectory frac")
+    close(lat, g["lattices"], what="trajectory lattices")
+
+
+def test_sample_api_returns_sorted_structures(model100, golden, cn):
+    torch.manual_seed(42)
+    atoms = model100.sample(None, 6, 4, text_embeds=cn[0], null_text_embeds=cn[1])
+    g = golden("trajectory_4x6_T100.npz")
+    nums = np.concatenate([np.asarray(at.numbers) for at in atoms])
+    np.testing.assert_array_equal(nums, g["final_sorted_numbers"])
+
+
+# --------------------------------------------------------------------------- perf-mode properties
+def test_philox_shard_invariance(model100, cn):
+    """Perf-mode noise is keyed by global indices: sampling 6 crystals as one
+    batch or as two shards gives identical results."""
+    nat = [5, 9, 3, 12, 7, 4]
+    full = list(model100.sample_states(nat, None, 2.0, 1e-5, noise="philox", seed=7, text_embeds=cn[0],
+                                       null_text_embeds=cn[1], clone=False, t_stop=90))[-1]
+    g = torch.Generator().manual_seed(7)
+    l0 = torch.randn(6, 3, 3, generator=g) * model100.mask_lattice_matrix
+    x0 = torch.randn(sum(nat), 3, generator=g)
+    parts = []
+    for (g0, g1) in ((0, 2), (2, 6)):
+        n0, n1 = sum(nat[:g0]), sum(nat[:g1])
+        parts.append(list(model100.sample_states(nat[g0:g1], None, 2.0, 1e-5, noise="philox", seed=7,
+                                                 text_embeds=cn[0], null_text_embeds=cn[1], clone=False,
+                                                 t_stop=90, node_base=n0, graph_base=g0,
+                                                 init=(l0[g0:g1], x0[n0:n1])))[-1])
+    for k in (1, 2, 3):
+        cat = torch.cat([p[k] for p in parts])
+        assert torch.equal(cat, full[k]), f"state {k} differs between 1 and 2 shards"
+
+
+def test_large_batch_step_is_finite(model1000, cn):
+    """512 x 40 (BASELINE metric shape): one reverse step in perf mode."""
+    nat = [40] * 512
+    N = sum(nat)
+    a = torch.zeros(N, dtype=torch.long)
+    x = torch.rand(N, 3, generator=torch.Generator().manual_seed(1))
+    lat = torch.randn(512, 3, 3, generator=torch.Generator().manual_seed(2)) * model1000.mask_lattice_matrix
+    a2, x2, l2 = model1000.reverse_step(1000, a, x, lat, nat, 2.0, 1e-5, cn[0], cn[1], noise=None, seed=3)
+    assert torch.isfinite(x2).all() and torch.isfinite(l2).all()
+    assert ((a2 >= 0) & (a2 < 104)).all()
+    assert ((x2 >= 0) & (x2 <= 1)).all()
+    assert (l2.abs() <= 6).all()  # t == T clip
