@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark of the Chemeleon reverse-diffusion sampling path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): structures/sec of a 1000-step sample at n_atoms=40,
+n_samples=512 in total, at 1/2/4/8 GPUs (strong scaling: the 512 samples are
+split across ranks, 512/N each, contiguous ranges; samples are independent so
+there is no collective in the timed region).
+
+A "step" = one reverse-diffusion timestep over the rank's whole batch: the
+predictor classifier-free-guidance decoder pair, the D3PM / lattice / VE
+updates, the corrector pair and the Langevin update (chm_sample_step), with
+the state resident in HBM and device (Philox) noise. Every timestep has the
+same shapes, so structures/sec = n_samples / (T * seconds_per_step), T = 1000.
+Weights: the seeded synthetic recipe of the real architecture (hidden 512,
+6 layers, 128 frequencies, fc edges); conditioning: seeded vectors broadcast
+from rank 0 (RCCL), standing in for the frozen text encoder's output.
+
+One JSON line is printed by rank 0, including:
+  roofline     — the dominant kernel (edge message GEMM) against fp32 MFMA peak,
+                 timed live with HIP events on its launch stream;
+  msgpass      — the message-passing aggregation kernel against HBM peak;
+  cpu_baseline — the CPU oracle (a restatement of the reference PyTorch CPU
+                 path) timed on this host on a bounded sample (rank 0, N=1).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+T_STEPS = 1000
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
+H, FD, L, A = 512, 768, 6, 104
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n-samples", type=int, default=512, help="total samples across all ranks")
+    p.add_argument("--n-atoms", type=int, default=40)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-samples", type=int, default=8)
+    p.add_argument("--cpu-steps", type=int, default=2)
+    return p.parse_args()
+
+
+def decoder_pair_flops(natoms, P=2, share_fourier=True):
+    """Algorithmic fp32 flops of one decoder call pair as implemented
+    (SURVEY.md §8(d) factorised formula, with the Fourier projection shared
+    by the cond/null pair)."""
+    E = sum(n * n for n in natoms)
+    N = sum(natoms)
+    B = len(natoms)
+    edge = E * L * ((1 if share_fourier else P) * 2 * FD * H + P * 2 * H * H)
+    node = P * N * L * (4 * H * H + 2 * (2 * H * H + H * H) + 2 * H * H)
+    heads = P * N * 2 * H * 107 + P * B * 2 * 640 * 2 * H
+    return edge + node + heads
+
+
+def cpu_baseline(n_samples, n_atoms, steps):
+    """Time the oracle (CPU restatement of the reference path) on this host."""
+    from chemeleon_amd.config import default_config
+    from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
+    from oracle import chemeleon_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = default_config()
+    torch.manual_seed(0)
+    m = O.OracleModel(cfg, synthetic_state_dict(cfg))
+    cond, null = synthetic_text_embeds(512)
+    nat = torch.tensor([n_atoms] * n_samples)
+    B, N = n_samples, n_samples * n_atoms
+    n2g = torch.arange(B).repeat_interleave(nat)
+    g = torch.Generator().manual_seed(1)
+    a = torch.zeros(N, dtype=torch.long)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.randn(B, 3, 3, generator=g) * O.LATTICE_MASK
+    c, nl = cond.expand(B, -1), null.expand(B, -1)
+    with torch.no_grad():
+        nz = m.draw_noise(T_STEPS, N, B)
+        m.step(T_STEPS, a, x, lat, nat, n2g, c, nl, nz)  # warm-up
+        t0 = time.perf_counter()
+        for k in range(steps):
+            t = T_STEPS - 1 - k
+            nz = m.draw_noise(t, N, B)
+            a, x, lat, _ = m.step(t, a, x, lat, nat, n2g, c, nl, nz)
+        dt = (time.perf_counter() - t0) / steps
+    return {"value": n_samples / (dt * T_STEPS), "unit": "structures/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle (torch CPU restatement of the reference path) {n_samples}x{n_atoms} atoms, "
+                      f"{steps} timed reverse steps after 1 warm-up, {dt:.2f} s/step, extrapolated x{T_STEPS}",
+            "s_per_step": dt}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from chemeleon_amd import Chemeleon, _lib
+    from chemeleon_amd.config import default_config
+    from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
+
+    # shard: contiguous sample ranges, 512/N each
+    total = args.n_samples
+    per = [total // world + (1 if r < total % world else 0) for r in range(world)]
+    g0 = sum(per[:rank])
+    natoms = [args.n_atoms] * per[rank]
+    node_base = g0 * args.n_atoms
+
+    cfg = default_config()
+    torch.manual_seed(0)
+    model = Chemeleon(cfg)
+    model.decoder.load_state_dict(synthetic_state_dict(cfg))
+    model = model.to(dev).eval()
+    cond, null = synthetic_text_embeds(512)
+    cond, null = cond.to(dev), null.to(dev)
+    if dist is not None:  # text embedding computed once on rank 0, broadcast over RCCL
+        dist.broadcast(cond, 0)
+        dist.broadcast(null, 0)
+
+    it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
+                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0)
+    next(it)  # initial state
+    for _ in range(args.warmup):
+        next(it)
+    torch.cuda.synchronize()
+
+    _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
+    _lib.check(_lib.load().chm_prof_enable(1), "prof_enable")
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        state = next(it)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.check(_lib.load().chm_prof_enable(0), "prof_disable")
+    if dist is not None:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        # finished structures -> every rank (the all-gather of the sampler; outside the timed region)
+        from chemeleon_amd.distributed import gather_states
+        gather_states(state[1:], natoms)
+
+    s_per_step = elapsed / args.steps
+    value = total / (s_per_step * T_STEPS)
+
+    # live per-kernel timing (HIP events on the launch stream)
+    nmsg, ms_msg = _lib.prof_read(_lib.K_EDGE_MESSAGE)
+    nfou, ms_fou = _lib.prof_read(_lib.K_EDGE_FOURIER)
+    nseg, ms_seg = _lib.prof_read(_lib.K_SEGMENT_MEAN)
+    ndec, ms_dec = _lib.prof_read(_lib.K_DECODER)
+    E = sum(n * n for n in natoms)
+    N = sum(natoms)
+    msg_flops = 2.0 * (2 * E) * H * H  # one launch covers both conditionings
+    msg_tflops = msg_flops / (ms_msg / nmsg * 1e-3) / 1e12 if nmsg else None
+    seg_bytes = 2.0 * (E * H * 4 + N * H * 4)
+    seg_gbs = seg_bytes / (ms_seg / nseg * 1e-3) / 1e9 if nseg else None
+    step_flops = 2 * decoder_pair_flops(natoms)
+
+    out = {
+        "metric": "structures/sec (1000-step sample, n_atoms=40)",
+        "value": value,
+        "unit": "structures/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": s_per_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded random-init weights of the real architecture; seeded conditioning vectors)",
+        "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
+                               f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
+                   "n_samples": total, "n_atoms": args.n_atoms, "timesteps": T_STEPS,
+                   "parallelism": f"sample-sharded x{world}", "noise": "philox (device)"},
+        "roofline": {"bound": "mfma", "kernel": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)",
+                     "achieved": msg_tflops, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": (msg_tflops / MFMA_F32_PEAK_TFLOPS) if msg_tflops else None, "traffic": None,
+                     "flops_per_launch": msg_flops, "launches": nmsg,
+                     "avg_ms": ms_msg / nmsg if nmsg else None},
+        "msgpass": {"bound": "hbm", "kernel": "k_segment_mean (scatter_mean of edge messages)",
+                    "achieved": seg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": (seg_gbs / HBM_PEAK_GBS) if seg_gbs else None, "bytes_per_launch": seg_bytes,
+                    "avg_ms": ms_seg / nseg if nseg else None},
+        "path": {"tflops": step_flops / s_per_step / 1e12, "mfma_frac": step_flops / s_per_step / 1e12 /
+                 MFMA_F32_PEAK_TFLOPS, "flops_per_step_per_gpu": step_flops,
+                 "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,
+                 "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_samples, args.n_atoms, args.cpu_steps)
+        except Exception as e:  # noqa: BLE001
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

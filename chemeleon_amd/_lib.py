@@ -56,6 +56,9 @@ SIGNATURES = {
     "chm_d3pm_sample": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     "chm_edge_features": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "chm_prof_enable": (c_int, [c_int]),
+    "chm_prof_reset": (c_int, []),
+    "chm_prof_read": (c_int, [c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
 }
 
 
@@ -104,3 +107,14 @@ def require_device(*tensors):
             raise RuntimeError("chemeleon_amd runs on a HIP device only: got a CPU tensor (no CPU fallback)")
         if not t.is_contiguous():
             raise RuntimeError("chemeleon_amd expects contiguous tensors")
+
+
+K_EDGE_FOURIER, K_EDGE_MESSAGE, K_SEGMENT_MEAN, K_DECODER = 0, 1, 2, 3
+
+
+def prof_read(kernel: int):
+    """(launches, total_ms) recorded for `kernel` since the last reset."""
+    n = c_i64()
+    ms = ctypes.c_double()
+    check(load().chm_prof_read(kernel, ctypes.byref(n), ctypes.byref(ms)), "chm_prof_read")
+    return int(n.value), float(ms.value)

@@ -290,6 +290,61 @@ extern "C" size_t chm_batch_device_bytes(const chm_batch* b) { return b ? b->byt
 extern "C" int64_t chm_batch_num_nodes(const chm_batch* b) { return b ? b->N : -1; }
 extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -1; }
 
+// ---------------------------------------------------------------- instrumentation
+namespace {
+struct ProfRec { int id; hipEvent_t a, b; };
+bool g_prof_on = false;
+std::vector<hipEvent_t> g_pool;
+std::vector<ProfRec> g_recs;
+size_t g_pool_next = 0;
+constexpr size_t kPoolPairs = 8192;
+
+struct ProfScope {
+  int id; hipStream_t s; hipEvent_t b = nullptr;
+  ProfScope(int id_, hipStream_t s_) : id(id_), s(s_) {
+    if (!g_prof_on || g_pool_next + 2 > g_pool.size()) return;
+    hipEvent_t a = g_pool[g_pool_next++];
+    b = g_pool[g_pool_next++];
+    if (hipEventRecord(a, s) != hipSuccess) { b = nullptr; return; }
+    g_recs.push_back({id, a, b});
+  }
+  ~ProfScope() { if (b) (void)hipEventRecord(b, s); }
+};
+}  // namespace
+
+extern "C" int chm_prof_enable(int on) {
+  if (on && g_pool.empty()) {
+    g_pool.resize(2 * kPoolPairs);
+    for (auto& e : g_pool)
+      if (hipEventCreate(&e) != hipSuccess) return fail(CHM_E_HIP, "hipEventCreate failed");
+  }
+  g_prof_on = on != 0;
+  return CHM_OK;
+}
+
+extern "C" int chm_prof_reset(void) {
+  g_recs.clear();
+  g_pool_next = 0;
+  return CHM_OK;
+}
+
+extern "C" int chm_prof_read(int kernel, int64_t* launches, double* total_ms) {
+  if (!launches || !total_ms) return fail(CHM_E_ARG, "NULL argument");
+  int64_t n = 0;
+  double tot = 0;
+  for (const auto& r : g_recs) {
+    if (r.id != kernel) continue;
+    float ms = 0;
+    hipError_t e = hipEventElapsedTime(&ms, r.a, r.b);
+    if (e != hipSuccess) return fail(CHM_E_HIP, std::string("hipEventElapsedTime: ") + hipGetErrorString(e));
+    ++n;
+    tot += ms;
+  }
+  *launches = n;
+  *total_ms = tot;
+  return CHM_OK;
+}
+
 static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const float* W, float* C, long ldc) {
   GemmArgs g;
   std::memset(&g, 0, sizeof(g));
@@ -305,6 +360,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   const int L = m->d.num_layers, X = m->d.text_dim, B = b->B;
   const long N = b->N, E = b->E, R = (long)P * N;
   const int CIN = TD + X;
+  ProfScope whole(CHM_K_DECODER, s);
   HIPCHK(build_cond_in(temb, tstride, text0, text1, X, b->cin, B, P, s));
   {
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
@@ -331,14 +387,19 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
       GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
       g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
+      ProfScope ps(CHM_K_EDGE_FOURIER, s);
       HIPCHK(gemm(g, EPI_EDGE, s));
     }
     {  // edge layer 2: M = SiLU(S W2^T + b2)
       GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
       g.bias = w.b2; g.act = 1;
+      ProfScope ps(CHM_K_EDGE_MESSAGE, s);
       HIPCHK(gemm(g, EPI_STD, s));
     }
-    HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
+    {
+      ProfScope ps(CHM_K_SEGMENT_MEAN, s);
+      HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
+    }
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);
       g.A2 = b->agg; g.lda2 = H; g.ksplit = H; g.bias = w.b3; g.act = 1;

@@ -153,6 +153,22 @@ int chm_d3pm_sample(int N, int A, int T, const float* d_logits, const int64_t* d
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */
 int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* stream);
 
+/* Bench instrumentation: while enabled, the runtime brackets every launch of
+ * the kernels below with HIP events on the launch stream (a pool of 8192
+ * pairs; recording stops when it is exhausted). After synchronising the
+ * device, chm_prof_read returns the launch count and summed duration.
+ *   CHM_K_EDGE_FOURIER  edge layer 1 (Fourier projection + node terms + SiLU)
+ *   CHM_K_EDGE_MESSAGE  edge layer 2 (message GEMM + SiLU)
+ *   CHM_K_SEGMENT_MEAN  message-passing aggregation (scatter_mean)
+ *   CHM_K_DECODER       one whole decoder call (all its kernels) */
+#define CHM_K_EDGE_FOURIER 0
+#define CHM_K_EDGE_MESSAGE 1
+#define CHM_K_SEGMENT_MEAN 2
+#define CHM_K_DECODER 3
+int chm_prof_enable(int on);
+int chm_prof_reset(void);
+int chm_prof_read(int kernel, int64_t* launches, double* total_ms);
+
 /* Sizes of the batch (for callers that allocate outputs). */
 int64_t chm_batch_num_nodes(const chm_batch* b);
 int64_t chm_batch_num_edges(const chm_batch* b);
