@@ -42,6 +42,8 @@ SIGNATURES = {
     "chm_model_create": (c_int, [ctypes.POINTER(chm_dims), ctypes.POINTER(c_void_p), c_int, c_void_p,
                                  ctypes.POINTER(c_void_p)]),
     "chm_model_destroy": (None, [c_void_p]),
+    "chm_model_set_math": (c_int, [c_void_p, c_int]),
+    "chm_model_get_math": (c_int, [c_void_p]),
     "chm_batch_create": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, ctypes.POINTER(c_void_p)]),
     "chm_batch_destroy": (None, [c_void_p]),
     "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
@@ -109,6 +111,7 @@ def require_device(*tensors):
             raise RuntimeError("chemeleon_amd expects contiguous tensors")
 
 
+MATH_BF16X3, MATH_F32 = 0, 1
 K_EDGE_FOURIER, K_EDGE_MESSAGE, K_SEGMENT_MEAN, K_DECODER = 0, 1, 2, 3
 
 

@@ -25,11 +25,22 @@ struct GemmArgs {
   int act;                                 // 0 = identity, 1 = SiLU
   // EPI_EDGE: S[c][e][n] = silu(acc + PQ[c*N + ei[e]][n] + PQ[c*N + ej[e]][H + n])
   const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
+  // bf16x3 path: W split into three bf16 planes [3][N][K] (hi, mid, lo)
+  const void* Wp3;
+  // EPI_SEGMEAN (message GEMM + scatter_mean): row tiles cover whole nodes
+  const int2* tiles; int ntiles;          // node ranges [x, y) of one conditioning
+  const long* node_estart;                // first edge row of each node
+  const int* natoms; const int* n2g;
+  float* agg;                             // [P][N][H]
 };
 
-enum { EPI_STD = 0, EPI_EDGE = 1 };
+enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 
 hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
+// fp32-accurate GEMM on bf16 MFMA: A split on the fly into hi/mid/lo bf16,
+// W pre-split; six products per fp32 product, fp32 accumulation.
+hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s);
+hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 
 hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* F, hipStream_t s);
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,

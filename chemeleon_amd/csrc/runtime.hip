@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,13 +34,19 @@ static int fail(int code, const std::string& msg) {
 
 struct LayerW {
   const float *WAB, *Wcl, *b1, *D, *W2, *b2, *W3, *b3, *W4, *b4, *lw, *lb;
+  const void *WAB3, *D3, *W23, *W33, *W43;  // bf16 hi/mid/lo planes of the GEMM weights
 };
+
+enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1 };
 
 struct chm_model {
   chm_dims d;
   float* mem = nullptr;
   size_t mem_floats = 0;
   const float *emb, *Wc, *bc, *Wp, *bp, *fw, *fb, *Whead, *bhead, *Wlat, *flw, *flb;
+  const void *Wc3, *Wp3, *Whead3;
+  void* mem3 = nullptr;  // bf16 planes arena
+  int math = MATH_BF16X3;
   std::vector<LayerW> layers;
 };
 
@@ -50,7 +57,10 @@ struct chm_batch {
   std::vector<int> h_natoms;
   // index tables
   int *natoms, *node_off, *n2g, *ei, *ej;
-  long* edge_off;
+  long *edge_off, *node_estart;
+  int2* tiles;  // node ranges [x, y) whose edge rows fit one 128-row GEMM tile
+  int ntiles;
+  int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
   std::vector<void*> allocs;
@@ -58,7 +68,7 @@ struct chm_batch {
 };
 
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
-extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.1 (gfx950, fp32 MFMA)"; }
+extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.2 (gfx950; bf16x3-split or f32 MFMA)"; }
 
 extern "C" int chm_num_params(const chm_dims* d) { return d ? 7 + 10 * d->num_layers + 6 : 0; }
 
@@ -180,13 +190,65 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     w.b2 = base + o[5]; w.W3 = base + o[6]; w.b3 = base + o[7]; w.W4 = base + o[8]; w.b4 = base + o[9];
     w.lw = base + o[10]; w.lb = base + o[11];
   }
+  // bf16x3 planes of every GEMM weight (fp32-accurate bf16 MFMA path)
+  {
+    const char* env = getenv("CHM_MATH");
+    m->math = (env && std::string(env) == "f32") ? MATH_F32 : MATH_BF16X3;
+    struct Job { const float* src; size_t n; const void** dst; };
+    std::vector<Job> jobs;
+    jobs.push_back({m->Wc, (size_t)2 * H * CIN, &m->Wc3});
+    jobs.push_back({m->Wp, (size_t)H * H, &m->Wp3});
+    jobs.push_back({m->Whead, (size_t)HEADS_N * H, &m->Whead3});
+    for (auto& w : m->layers) {
+      jobs.push_back({w.WAB, (size_t)2 * H * H, &w.WAB3});
+      jobs.push_back({w.D, (size_t)H * FD, &w.D3});
+      jobs.push_back({w.W2, (size_t)H * H, &w.W23});
+      jobs.push_back({w.W3, (size_t)H * 2 * H, &w.W33});
+      jobs.push_back({w.W4, (size_t)H * H, &w.W43});
+    }
+    size_t total = 0;
+    for (auto& j : jobs) total += (3 * j.n * 2 + 255) / 256 * 256;
+    hipError_t e2 = hipMalloc(&m->mem3, total);
+    if (e2 != hipSuccess) {
+      (void)hipFree(m->mem);
+      delete m;
+      return fail(CHM_E_HIP, std::string("hipMalloc(planes): ") + hipGetErrorString(e2));
+    }
+    char* p3 = (char*)m->mem3;
+    for (auto& j : jobs) {
+      *j.dst = p3;
+      hipError_t e3 = split_planes(j.src, (long)j.n, p3, s);
+      if (e3 != hipSuccess) {
+        (void)hipFree(m->mem); (void)hipFree(m->mem3);
+        delete m;
+        return fail(CHM_E_HIP, std::string("split_planes: ") + hipGetErrorString(e3));
+      }
+      p3 += (3 * j.n * 2 + 255) / 256 * 256;
+    }
+    e2 = hipStreamSynchronize(s);
+    if (e2 != hipSuccess) {
+      (void)hipFree(m->mem); (void)hipFree(m->mem3);
+      delete m;
+      return fail(CHM_E_HIP, std::string("plane split sync: ") + hipGetErrorString(e2));
+    }
+  }
   *out = m;
   return CHM_OK;
 }
 
+extern "C" int chm_model_set_math(chm_model* m, int mode) {
+  if (!m) return fail(CHM_E_ARG, "model is NULL");
+  if (mode != CHM_MATH_BF16X3 && mode != CHM_MATH_F32) return fail(CHM_E_ARG, "unknown math mode");
+  m->math = mode;
+  return CHM_OK;
+}
+
+extern "C" int chm_model_get_math(const chm_model* m) { return m ? m->math : -1; }
+
 extern "C" void chm_model_destroy(chm_model* m) {
   if (!m) return;
   (void)hipFree(m->mem);
+  (void)hipFree(m->mem3);
   delete m;
 }
 
@@ -219,8 +281,28 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
         ej[e] = noff[g] + j;
       }
   }
+  std::vector<long> estart(N);
+  std::vector<int2> tiles;
+  {
+    int cur0 = 0;
+    long rows = 0;
+    for (int g = 0; g < B; ++g)
+      for (int i = 0; i < nat[g]; ++i) {
+        const int node = noff[g] + i;
+        estart[node] = eoff[g] + (long)i * nat[g];
+        if (nat[g] > 128) return fail(CHM_E_UNSUPPORTED, "crystals above 128 atoms are not supported");
+        if (rows + nat[g] > 128) {
+          tiles.push_back(make_int2(cur0, node));
+          cur0 = node;
+          rows = 0;
+        }
+        rows += nat[g];
+      }
+    tiles.push_back(make_int2(cur0, (int)N));
+  }
   chm_batch* b = new chm_batch();
   b->m = m;
+  b->math = m->math;
   b->B = B;
   b->P = max_pairs;
   b->N = N;
@@ -246,7 +328,10 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->n2g = (int*)alloc(N * sizeof(int));
   b->ei = (int*)alloc(E * sizeof(int));
   b->ej = (int*)alloc(E * sizeof(int));
-  ok = b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej;
+  b->node_estart = (long*)alloc(N * sizeof(long));
+  b->tiles = (int2*)alloc(tiles.size() * sizeof(int2));
+  b->ntiles = (int)tiles.size();
+  ok = b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej && b->node_estart && b->tiles;
   b->cin = fl((size_t)P * B * (TD + X));
   b->cemb = fl((size_t)P * B * 2 * H);
   b->Hres = fl((size_t)P * N * H);
@@ -257,7 +342,7 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->gbias = fl((size_t)L * B * H);
   b->F = fl((size_t)E * FD);
   b->S = fl((size_t)P * E * H);
-  b->M = fl((size_t)P * E * H);
+  b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
   b->LAT = fl((size_t)P * B * 9);
@@ -272,6 +357,8 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   if (e == hipSuccess) e = hipMemcpy(b->n2g, n2g.data(), N * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(b->ei, ei.data(), E * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(b->ej, ej.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->node_estart, estart.data(), N * sizeof(long), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     chm_batch_destroy(b);
     return fail(CHM_E_HIP, std::string("index upload: ") + hipGetErrorString(e));
@@ -353,6 +440,12 @@ static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const floa
   return g;
 }
 
+static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
+  if (b->math == MATH_F32) return gemm(g, epi, s);
+  g.Wp3 = W3;
+  return gemm_bf16x3(g, epi, s);
+}
+
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
                        int tstride, const float* text0, const float* text1, int heads, hipStream_t s) {
@@ -365,7 +458,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   {
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
-    HIPCHK(gemm(g, EPI_STD, s));
+    HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
   HIPCHK(embed(a, m->emb, b->Hres, N, P, s));
   HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
@@ -376,46 +469,52 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     {  // FiLM projection (cspnet.py:92)
       GemmArgs g = gargs(R, H, H, b->Hres, H, m->Wp, b->Y, H);
       g.bias = m->bp;
-      HIPCHK(gemm(g, EPI_STD, s));
+      HIPCHK(run_gemm(b, g, EPI_STD, m->Wp3, s));
     }
     HIPCHK(film_ln(b->Y, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s));
     {  // per-node halves of the first edge layer: [P | Q] = Hl [A ; Bm]^T, P += b1 + C vec(LL^T)
       GemmArgs g = gargs(R, 2 * H, H, b->Hl, H, w.WAB, b->PQ, 2 * H);
       g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
-      HIPCHK(gemm(g, EPI_STD, s));
+      HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s));
     }
     {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
       GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
       g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
       ProfScope ps(CHM_K_EDGE_FOURIER, s);
-      HIPCHK(gemm(g, EPI_EDGE, s));
+      HIPCHK(run_gemm(b, g, EPI_EDGE, w.D3, s));
     }
-    {  // edge layer 2: M = SiLU(S W2^T + b2)
-      GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
-      g.bias = w.b2; g.act = 1;
-      ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-      HIPCHK(gemm(g, EPI_STD, s));
-    }
-    {
+    if (b->math == MATH_F32) {
+      {  // edge layer 2: M = SiLU(S W2^T + b2)
+        GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
+        g.bias = w.b2; g.act = 1;
+        ProfScope ps(CHM_K_EDGE_MESSAGE, s);
+        HIPCHK(gemm(g, EPI_STD, s));
+      }
       ProfScope ps(CHM_K_SEGMENT_MEAN, s);
       HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
+    } else {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2), M never stored
+      GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, nullptr, H);
+      g.bias = w.b2; g.act = 1; g.tiles = b->tiles; g.ntiles = b->ntiles; g.node_estart = b->node_estart;
+      g.natoms = b->natoms; g.n2g = b->n2g; g.agg = b->agg; g.nnodes = N; g.npairs = P; g.E = E;
+      ProfScope ps(CHM_K_EDGE_MESSAGE, s);
+      HIPCHK(run_gemm(b, g, EPI_SEGMEAN, w.W23, s));
     }
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);
       g.A2 = b->agg; g.lda2 = H; g.ksplit = H; g.bias = w.b3; g.act = 1;
-      HIPCHK(gemm(g, EPI_STD, s));
+      HIPCHK(run_gemm(b, g, EPI_STD, w.W33, s));
     }
     {  // node MLP 2 + residual: Hres += SiLU(U W4^T + b4)
       GemmArgs g = gargs(R, H, H, b->Y, H, w.W4, b->Hres, H);
       g.bias = w.b4; g.act = 1; g.R = b->Hres; g.ldr = H;
-      HIPCHK(gemm(g, EPI_STD, s));
+      HIPCHK(run_gemm(b, g, EPI_STD, w.W43, s));
     }
   }
   HIPCHK(layer_norm(b->Hres, b->Hf, R, m->flw, m->flb, s));
   if (heads & 1) {
     GemmArgs g = gargs(R, HEADS_N, H, b->Hf, H, m->Whead, b->HO, HEADS_N);
     g.bias = m->bhead;
-    HIPCHK(gemm(g, EPI_STD, s));
+    HIPCHK(run_gemm(b, g, EPI_STD, m->Whead3, s));
   }
   if (heads & 2) HIPCHK(graph_heads(b->Hf, m->Wlat, lat, b->node_off, b->natoms, N, B, P, b->LAT, s));
   return CHM_OK;

@@ -78,6 +78,19 @@ int chm_model_create(const chm_dims* dims, const float* const* d_params, int n_p
                      chm_model** out);
 void chm_model_destroy(chm_model* m);
 
+/* Arithmetic of the decoder GEMMs (both fp32-accurate):
+ *   CHM_MATH_BF16X3 (default): each fp32 operand split into three bf16 parts,
+ *     six bf16 MFMA products per fp32 product, fp32 accumulation; the edge
+ *     message GEMM is fused with the scatter_mean aggregation.
+ *   CHM_MATH_F32: v_mfma_f32_32x32x2_f32 (exact fp32 fma chains); standalone
+ *     aggregation kernel.
+ * The environment variable CHM_MATH=f32 selects the latter at creation.
+ * A batch keeps the mode its model had when the batch was created. */
+#define CHM_MATH_BF16X3 0
+#define CHM_MATH_F32 1
+int chm_model_set_math(chm_model* m, int mode);
+int chm_model_get_math(const chm_model* m);
+
 /* Describes a (possibly ragged) batch of crystals and owns the workspace of
  * its decoder calls. Replaces: Batch.from_data_list + the fc edge builder
  * (chemeleon.py:335-343, cspnet.py:319-324): node i of crystal g is global

@@ -104,8 +104,13 @@ def test_d3pm_bit_exact(model100, golden):
 
 
 # --------------------------------------------------------------------------- decoder
+MATHS = ["bf16x3", "f32"]
+
+
+@pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("name", ["decoder_4x6.npz", "decoder_ragged.npz"])
-def test_decoder_forward(model1000, golden, name, cn):
+def test_decoder_forward(model1000, golden, name, cn, math):
+    model1000.decoder.set_math(math)
     g = golden(name)
     sd = model1000.decoder.state_dict()
     assert weights_crc({k: v.cpu() for k, v in sd.items()}) == int(g["weights_crc"])
@@ -138,9 +143,11 @@ def test_cfg_pair(model1000, golden, cn):
 
 
 # --------------------------------------------------------------------------- sampler
+@pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("tag", ["64x20", "16x40"])
-def test_teacher_forced_steps(model1000, golden, cn, tag):
+def test_teacher_forced_steps(model1000, golden, cn, tag, math):
     """Reference state at t + the reference's noise stream -> state at t-1."""
+    model1000.decoder.set_math(math)
     g = golden(f"step_{tag}.npz")
     nat = g["natoms"].tolist()
     B, N = len(nat), sum(nat)
@@ -158,8 +165,10 @@ def test_teacher_forced_steps(model1000, golden, cn, tag):
         close(lat.cpu(), g[f"t{t}_l_out"], what=f"lattice t={t}")
 
 
-def test_trajectory_c0(model100, golden, cn):
+@pytest.mark.parametrize("math", MATHS)
+def test_trajectory_c0(model100, golden, cn, math):
     """C0 (configs[0]): 4 x 6 atoms, T = 100, seed 42, the full sampler."""
+    model100.decoder.set_math(math)
     g = golden("trajectory_4x6_T100.npz")
     torch.manual_seed(42)
     states = list(model100.sample_states([6] * 4, None, 2.0, 1e-5, noise="torch", text_embeds=cn[0],
@@ -170,6 +179,53 @@ def test_trajectory_c0(model100, golden, cn):
     np.testing.assert_array_equal(a, g["atom_types"])
     periodic_close(x, g["frac"], what="trajectory frac")
     close(lat, g["lattices"], what="trajectory lattices")
+
+
+def test_decoder_large_ragged_vs_oracle(model1000, cn):
+    """Crystals from 1 to 80 atoms (stress-config sizes) in one batch, both
+    conditionings, against the CPU oracle."""
+    nat = [80, 1, 37, 64, 2, 80, 13]
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(17)
+    a = torch.randint(0, 104, (N,), generator=g)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.randn(B, 3, 3, generator=g) * 4
+    te = model1000.time_embed(torch.full((B,), 321, dtype=torch.long))
+    sd = {k: v.detach().cpu() for k, v in model1000.decoder.state_dict().items()}
+    nat_t = torch.tensor(nat)
+    n2g = torch.arange(B).repeat_interleave(nat_t)
+    for math in MATHS:
+        model1000.decoder.set_math(math)
+        types, latt, coords, nodes = model1000.decoder.forward_cfg(a.to(DEV), x.to(DEV), lat.to(DEV), nat_t.to(DEV),
+                                                                   te.to(DEV), cn[0].expand(B, -1).to(DEV),
+                                                                   cn[1].expand(B, -1).to(DEV), need_nodes=True)
+        for c, text in enumerate(cn):
+            rt, rl, rc, rh = O.cspnet_forward(sd, default_config(), a, x, lat, nat_t, n2g, te, text.expand(B, -1))
+            close(nodes[c].cpu(), rh, what=f"{math} nodes c={c}")
+            close(types[c].cpu(), rt, what=f"{math} types c={c}")
+            close(coords[c].cpu(), rc, what=f"{math} coords c={c}")
+            close(latt[c].cpu(), rl, what=f"{math} lattice c={c}")
+
+
+def test_bf16x3_matches_f32_path(model1000, cn):
+    """The two GEMM arithmetics agree to fp32 rounding level on 64 x 20."""
+    nat = [20] * 64
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(23)
+    a = torch.randint(0, 104, (N,), generator=g).to(DEV)
+    x = torch.rand(N, 3, generator=g).to(DEV)
+    lat = (torch.randn(B, 3, 3, generator=g) * 4).to(DEV)
+    te = model1000.time_embed(torch.full((B,), 500, dtype=torch.long)).to(DEV)
+    nat_t = torch.tensor(nat).to(DEV)
+    outs = {}
+    for math in MATHS:
+        model1000.decoder.set_math(math)
+        outs[math] = model1000.decoder.forward_cfg(a, x, lat, nat_t, te, cn[0].expand(B, -1).to(DEV),
+                                                   cn[1].expand(B, -1).to(DEV), need_nodes=True)
+    for k, name in enumerate(["types", "lattice", "coords", "nodes"]):
+        err = close(outs["bf16x3"][k].cpu(), outs["f32"][k].cpu(), rtol=2e-5, what=name)
+        print(f"bf16x3 vs f32 {name}: max scaled err {err:.2e}")
+    model1000.decoder.set_math("bf16x3")
 
 
 def test_sample_api_returns_sorted_structures(model100, golden, cn):
