@@ -40,7 +40,10 @@ hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
 // fp32-accurate GEMM on bf16 MFMA: A split on the fly into hi/mid/lo bf16,
 // W pre-split; six products per fp32 product, fp32 accumulation.
 hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s);
+// 256x256-tile variant (edge GEMMs); EPI_SEGMEAN tiles must then hold <= 256 rows
+hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s);
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
+extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
 
 hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* F, hipStream_t s);
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,

@@ -38,6 +38,7 @@ struct LayerW {
 };
 
 enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1 };
+constexpr long kTileRows = 256;  // rows of the edge-GEMM tiles (gemm_bf16x3_big)
 
 struct chm_model {
   chm_dims d;
@@ -58,7 +59,7 @@ struct chm_batch {
   // index tables
   int *natoms, *node_off, *n2g, *ei, *ej;
   long *edge_off, *node_estart;
-  int2* tiles;  // node ranges [x, y) whose edge rows fit one 128-row GEMM tile
+  int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
@@ -290,8 +291,8 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
       for (int i = 0; i < nat[g]; ++i) {
         const int node = noff[g] + i;
         estart[node] = eoff[g] + (long)i * nat[g];
-        if (nat[g] > 128) return fail(CHM_E_UNSUPPORTED, "crystals above 128 atoms are not supported");
-        if (rows + nat[g] > 128) {
+        if (nat[g] > kTileRows) return fail(CHM_E_UNSUPPORTED, "crystals above 256 atoms are not supported");
+        if (rows + nat[g] > kTileRows) {
           tiles.push_back(make_int2(cur0, node));
           cur0 = node;
           rows = 0;
@@ -446,6 +447,13 @@ static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* 
   return gemm_bf16x3(g, epi, s);
 }
 
+// the two edge GEMMs (M = E or P*E rows): 256x256 tiles in bf16x3 mode
+static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
+  if (b->math == MATH_F32) return gemm(g, epi, s);
+  g.Wp3 = W3;
+  return gemm_bf16x3_big(g, epi, s);
+}
+
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
                        int tstride, const float* text0, const float* text1, int heads, hipStream_t s) {
@@ -481,7 +489,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
       g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
       ProfScope ps(CHM_K_EDGE_FOURIER, s);
-      HIPCHK(run_gemm(b, g, EPI_EDGE, w.D3, s));
+      HIPCHK(run_edge_gemm(b, g, EPI_EDGE, w.D3, s));
     }
     if (b->math == MATH_F32) {
       {  // edge layer 2: M = SiLU(S W2^T + b2)
@@ -497,7 +505,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       g.bias = w.b2; g.act = 1; g.tiles = b->tiles; g.ntiles = b->ntiles; g.node_estart = b->node_estart;
       g.natoms = b->natoms; g.n2g = b->n2g; g.agg = b->agg; g.nnodes = N; g.npairs = P; g.E = E;
       ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-      HIPCHK(run_gemm(b, g, EPI_SEGMEAN, w.W23, s));
+      HIPCHK(run_edge_gemm(b, g, EPI_SEGMEAN, w.W23, s));
     }
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);

@@ -1,0 +1,97 @@
+// Standalone microbenchmark of the decoder GEMM kernels (edge shapes at 512x40).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_bench.cpp chemeleon_amd/csrc/kernels.hip \
+//         chemeleon_amd/csrc/gemm_bf16x3.hip -o tools/gemm_bench && tools/gemm_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <functional>
+#include <cmath>
+
+#include "../chemeleon_amd/csrc/chm_internal.h"
+
+using namespace chm;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void fill(float* p, long n, unsigned seed, float scale) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned x = (unsigned)(i * 2654435761u) ^ seed;
+  x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+  p[i] = ((x & 0xFFFFFF) / 16777216.0f - 0.5f) * scale;
+}
+
+static float time_it(int reps, hipStream_t s, const std::function<void()>& f) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f();
+  CK(hipStreamSynchronize(s));
+  CK(hipEventRecord(a, s));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+int main(int argc, char** argv) {
+  const long M = argc > 1 ? atol(argv[1]) : 2L * 819200;  // rows (2E for the message GEMM)
+  const int N = 512;
+  const int K = argc > 2 ? atoi(argv[2]) : 512;
+  hipStream_t s; CK(hipStreamCreate(&s));
+  float *A, *W, *C, *bias;
+  void* W3;
+  CK(hipMalloc(&A, M * K * 4)); CK(hipMalloc(&W, (long)N * K * 4)); CK(hipMalloc(&C, M * N * 4));
+  CK(hipMalloc(&bias, N * 4)); CK(hipMalloc(&W3, 3L * N * K * 2));
+  fill<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, 1, 2.0f);
+  fill<<<(N * K + 255) / 256, 256, 0, s>>>(W, (long)N * K, 2, 0.1f);
+  fill<<<(N + 255) / 256, 256, 0, s>>>(bias, N, 3, 0.1f);
+  CK(split_planes(W, (long)N * K, W3, s));
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.A2 = A; g.lda2 = K; g.ksplit = K;
+  g.W = W; g.ldw = K; g.C = C; g.ldc = N; g.bias = bias; g.act = 1; g.gb_rowmod = 1; g.Wp3 = W3;
+  const double flops = 2.0 * M * N * K;
+  float t32 = time_it(5, s, [&] { CK(gemm(g, EPI_STD, s)); });
+  printf("M=%ld N=%d K=%d  f32-mfma: %.3f ms %.1f TF\n", M, N, K, t32, flops / t32 / 1e9);
+  for (int v = 0; v < 4; ++v) {
+    g_gemm3_variant = v;
+    float t3 = time_it(5, s, [&] { CK(gemm_bf16x3(g, EPI_STD, s)); });
+    printf("  bf16x3 variant %d (prefetch %d, xcd remap %d): %.3f ms %.1f TF fp32-equivalent\n", v, (v & 1) + 1,
+           (v >> 1) & 1, t3, flops / t3 / 1e9);
+  }
+  g_gemm3_variant = 3;
+  {
+    float tb = time_it(5, s, [&] { CK(gemm_bf16x3_big(g, EPI_STD, s)); });
+    printf("  bf16x3 big (256x256, 8 waves): %.3f ms %.1f TF fp32-equivalent\n", tb, flops / tb / 1e9);
+    std::vector<float> c1(65536 * 4), c2(65536 * 4);
+    CK(gemm_bf16x3(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
+    CK(gemm_bf16x3_big(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0;
+    for (size_t i = 0; i < c1.size(); ++i) mx = fmax(mx, fabs((double)c1[i] - c2[i]));
+    printf("  max |big - small| = %.3e\n", mx);
+  }
+  // accuracy of bf16x3 against the f32-MFMA result
+  std::vector<float> c32(M > 65536 ? 65536 * N : M * N), c3(c32.size());
+  CK(gemm(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
+  CK(hipMemcpy(c32.data(), C, c32.size() * 4, hipMemcpyDeviceToHost));
+  CK(gemm_bf16x3(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
+  CK(hipMemcpy(c3.data(), C, c3.size() * 4, hipMemcpyDeviceToHost));
+  double mx = 0, ms = 0;
+  for (size_t i = 0; i < c32.size(); ++i) {
+    double d = fabs((double)c3[i] - c32[i]);
+    mx = d > mx ? d : mx; ms += (double)c32[i] * c32[i];
+  }
+  printf("max |bf16x3 - f32| = %.3e (rms value %.3e)\n", mx, sqrt(ms / c32.size()));
+  return 0;
+}
