@@ -40,6 +40,10 @@ sys.path.insert(0, REPO)
 
 T_STEPS = 1000
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA peak (spec)
+# bf16x3 arithmetic: six bf16 MFMA products per fp32-accurate product, so the
+# ceiling for fp32-equivalent flops on the bf16 pipe is 2.5 PF / 6
+BF16X3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
 H, FD, L, A = 512, 768, 6, 104
 
@@ -55,6 +59,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-samples", type=int, default=8)
     p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--math", choices=["bf16x3", "f32"], default="bf16x3",
+                   help="decoder GEMM arithmetic (both fp32-accurate; see include/chemeleon_hip.h)")
     return p.parse_args()
 
 
@@ -141,6 +147,7 @@ def main():
         dist.broadcast(cond, 0)
         dist.broadcast(null, 0)
 
+    model.decoder.set_math(args.math)
     it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
                              null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0)
     next(it)  # initial state
@@ -175,15 +182,38 @@ def main():
     # live per-kernel timing (HIP events on the launch stream)
     nmsg, ms_msg = _lib.prof_read(_lib.K_EDGE_MESSAGE)
     nfou, ms_fou = _lib.prof_read(_lib.K_EDGE_FOURIER)
-    nseg, ms_seg = _lib.prof_read(_lib.K_SEGMENT_MEAN)
     ndec, ms_dec = _lib.prof_read(_lib.K_DECODER)
     E = sum(n * n for n in natoms)
     N = sum(natoms)
     msg_flops = 2.0 * (2 * E) * H * H  # one launch covers both conditionings
     msg_tflops = msg_flops / (ms_msg / nmsg * 1e-3) / 1e12 if nmsg else None
     seg_bytes = 2.0 * (E * H * 4 + N * H * 4)
-    seg_gbs = seg_bytes / (ms_seg / nseg * 1e-3) / 1e9 if nseg else None
     step_flops = 2 * decoder_pair_flops(natoms)
+    math = model.decoder.get_math()
+    peak = BF16X3_PEAK_TFLOPS if math == "bf16x3" else MFMA_F32_PEAK_TFLOPS
+
+    # standalone message-passing aggregation kernel (chm_segment_mean) on the
+    # bench batch's edge layout, [2, E, 512] fp32 messages (HIP events)
+    seg_gbs = seg_ms = None
+    try:
+        b = model.decoder.hip_batch(natoms, 2)
+        msg = torch.empty(2, b.num_edges, H, device=dev).normal_()
+        agg = torch.empty(2, b.num_nodes, H, device=dev)
+        L_ = _lib.load()
+        st = _lib.stream_handle(dev)
+        for _ in range(2):
+            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), _lib.ptr(agg), st), "segment_mean")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), _lib.ptr(agg), st), "segment_mean")
+        e1.record()
+        torch.cuda.synchronize()
+        seg_ms = e0.elapsed_time(e1) / 10
+        seg_gbs = seg_bytes / (seg_ms * 1e-3) / 1e9
+        del msg, agg
+    except Exception as e:  # noqa: BLE001
+        print("segment_mean microbench failed:", repr(e), file=sys.stderr)
 
     out = {
         "metric": "structures/sec (1000-step sample, n_atoms=40)",
@@ -196,23 +226,30 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if math == "f32" else "f32 (bf16x3-split MFMA, fp32 accumulate)",
         "data": "synthetic (seeded random-init weights of the real architecture; seeded conditioning vectors)",
         "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
                    "n_samples": total, "n_atoms": args.n_atoms, "timesteps": T_STEPS,
                    "parallelism": f"sample-sharded x{world}", "noise": "philox (device)"},
-        "roofline": {"bound": "mfma", "kernel": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)",
-                     "achieved": msg_tflops, "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (msg_tflops / MFMA_F32_PEAK_TFLOPS) if msg_tflops else None, "traffic": None,
+        "roofline": {"bound": "mfma",
+                     "kernel": ("edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), both conditionings"
+                                if math == "bf16x3" else "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"),
+                     "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
+                     "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": None,
+                     "peak_note": ("fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products" if math == "bf16x3"
+                                   else "fp32 MFMA dense peak"),
                      "flops_per_launch": msg_flops, "launches": nmsg,
                      "avg_ms": ms_msg / nmsg if nmsg else None},
-        "msgpass": {"bound": "hbm", "kernel": "k_segment_mean (scatter_mean of edge messages)",
+        "msgpass": {"bound": "hbm", "kernel": "k_segment_mean (standalone scatter_mean, chm_segment_mean)",
                     "achieved": seg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": (seg_gbs / HBM_PEAK_GBS) if seg_gbs else None, "bytes_per_launch": seg_bytes,
-                    "avg_ms": ms_seg / nseg if nseg else None},
-        "path": {"tflops": step_flops / s_per_step / 1e12, "mfma_frac": step_flops / s_per_step / 1e12 /
-                 MFMA_F32_PEAK_TFLOPS, "flops_per_step_per_gpu": step_flops,
+                    "avg_ms": seg_ms,
+                    "note": ("in the sampler the aggregation is fused into the message GEMM epilogue; this is the "
+                             "standalone kernel on the same [2,E,512] shape" if math == "bf16x3" else
+                             "the kernel as launched by the sampler")},
+        "path": {"tflops": step_flops / s_per_step / 1e12, "mfma_frac": step_flops / s_per_step / 1e12 / peak,
+                 "math": math, "flops_per_step_per_gpu": step_flops,
                  "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,
                  "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
         "cpu_baseline": None,
