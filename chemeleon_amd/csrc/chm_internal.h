@@ -42,6 +42,7 @@ hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
 hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s);
 // 256x256-tile variant (edge GEMMs); EPI_SEGMEAN tiles must then hold <= 256 rows
 hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s);
+hipError_t gemm_init();  // one-time kernel attributes (call outside stream capture)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
 
@@ -49,8 +50,10 @@ hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* 
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,
                         const int* natoms, long N, long E, int P, hipStream_t s);
 hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s);
-hipError_t build_cond_in(const float* temb, int tstride, const float* text0, const float* text1, int text_dim, float* cin,
-                         int B, int P, hipStream_t s);
+// d_t != null: the time-embedding row is temb + (*d_t) * TD, shared by all graphs
+hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
+                         int text_dim, float* cin, int B, int P, hipStream_t s);
+hipError_t decrement(int* d_t, hipStream_t s);
 hipError_t graph_bias(const float* lat, const float* Wc, long ldwc, const float* b1, float* out, int B, hipStream_t s);
 hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
                    const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s);
@@ -62,6 +65,7 @@ hipError_t copy_rows(const float* src, long ld_src, float* dst, long ld_dst, lon
 
 struct StepArgs {
   int t, T, A;
+  const int* d_t;                  // if set, t is read from device memory (graph replay)
   long N; int B;
   float cs_null, cs_cond;          // (1 - s), s
   const float* coef;               // [T+1][8]
@@ -77,7 +81,8 @@ struct StepArgs {
 hipError_t step_predictor(const StepArgs& a, hipStream_t s);
 hipError_t step_corrector(const StepArgs& a, hipStream_t s);
 hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits, const float* logits2,
-                       float w1, float w2, const int64_t* xt, const int64_t* tnode, int t_const, const float* noise,
+                       float w1, float w2, const int64_t* xt, const int64_t* tnode, int t_const, const int* d_t,
+                       const float* noise,
                        const float* q1, const float* qm, int64_t* out, uint64_t seed, int64_t node_base,
                        hipStream_t s);
 

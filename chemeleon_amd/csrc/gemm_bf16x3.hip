@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs g) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[PA[t]][i], w[PW[t]][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[PW[t]][j], a[PA[t]][i], acc[i][j], 0, 0, 0);
   };
 
   const int nk = g.K / XBK;
@@ -186,65 +186,79 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs g) {
     }
   }
 
+  // accumulators hold C^T tiles (W fragments are the MFMA A operand): lane l owns
+  // output row wm*64 + i*32 + (l & 31) and, per 4-register group q, the four
+  // consecutive columns wn*64 + j*32 + 8q + 4h .. +3
   if (EPI == EPI_SEGMEAN) {
-    // messages m = SiLU(acc + b2) -> LDS tile [128][129] fp32 -> per-node column sums in
-    // edge order j = 0..n-1 (the reference's scatter_add_ order) -> mean -> agg
     float* T = reinterpret_cast<float*>(&smem[0][0]);
-    constexpr int TP = XBN + 1;
+    constexpr int TP = XBN + 4;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int q = 0; q < 4; ++q) {
+        const int col = wn * 64 + j * 32 + 8 * q + 4 * h;
+        const f32x4 b = *reinterpret_cast<const f32x4*>(g.bias + n0 + col);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int col = wn * 64 + j * 32 + r32;
-          T[row * TP + col] = silu3(acc[i][j][r] + g.bias[n0 + col]);
+        for (int i = 0; i < 2; ++i) {
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = silu_fast(acc[i][j][4 * q + e] + b[e]);
+          *reinterpret_cast<f32x4*>(T + (wm * 64 + i * 32 + r32) * TP + col) = v;
         }
+      }
     __syncthreads();
     const int col = tid & (XBN - 1);
     const long es0 = g.node_estart[seg.x];
     for (int nd = seg.x + (tid >> 7); nd < seg.y; nd += 2) {
       const int n = g.natoms[g.n2g[nd]];
       const int r0 = (int)(g.node_estart[nd] - es0);
-      float s = 0.f;
-      for (int j = 0; j < n; ++j) s += T[(r0 + j) * TP + col];
-      g.agg[((long)seg_c * g.nnodes + nd) * g.ldc + n0 + col] = s / (float)(n < 1 ? 1 : n);
+      float sacc = 0.f;
+      for (int j = 0; j < n; ++j) sacc += T[(r0 + j) * TP + col];
+      g.agg[((long)seg_c * g.nnodes + nd) * g.ldc + n0 + col] = sacc / (float)(n < 1 ? 1 : n);
     }
     return;
   }
 
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 64 + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+    if (EPI == EPI_EDGE) {
+      const long ii = g.ei[row], jj = g.ej[row];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const long lrow = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (lrow >= nrows) continue;
-      const long row = row0 + lrow;
-      if (EPI == EPI_EDGE) {
-        const long ii = g.ei[row], jj = g.ej[row];
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = n0 + wn * 64 + j * 32 + r32;
-          const float v = acc[i][j][r];
+        for (int q = 0; q < 4; ++q) {
+          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
           for (int c = 0; c < g.npairs; ++c) {
-            const float p = g.PQ[(c * g.nnodes + ii) * (2 * H) + col];
-            const float q = g.PQ[(c * g.nnodes + jj) * (2 * H) + H + col];
-            g.C[((long)c * g.E + row) * g.ldc + col] = silu3((v + p) + q);
+            const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+            const f32x4 p = *reinterpret_cast<const f32x4*>(Pc + ii * (2 * H) + col);
+            const f32x4 qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = silu_fast((acc[i][j][4 * q + e] + p[e]) + qv[e]);
+            *reinterpret_cast<f32x4*>(g.C + ((long)c * g.E + row) * g.ldc + col) = v;
           }
         }
-      } else {
+    } else {
+      const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = n0 + wn * 64 + j * 32 + r32;
-          float v = acc[i][j][r];
-          if (g.bias) v += g.bias[col];
-          if (g.gb && col < g.gb_cols) v += g.gb[(long)g.row2g[row % g.gb_rowmod] * g.ldgb + col];
-          if (g.act == 1) v = silu3(v);
-          if (g.R) v += g.R[row * g.ldr + col];
-          g.C[row * g.ldc + col] = v;
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+          if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+          if (g.act == 1)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = silu_fast(v[e]);
+          if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+          *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
         }
-      }
     }
   }
 }
@@ -453,6 +467,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
 
 constexpr size_t kBigLds = 2 * 6 * LPLANE * sizeof(__bf16);  // 147456 B
 
+// opt the 144 KB dynamic-LDS kernels in; called at model creation, outside any
+// stream capture (a function attribute call is not a stream operation)
+hipError_t gemm_init() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_gemm3_big<EPI_STD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kBigLds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm3_big<EPI_EDGE>, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm3_big<EPI_SEGMEAN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kBigLds);
+  return e;
+}
+
 hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.N % LBN || g.K % XBK || !g.Wp3 || g.ksplit % XBK || g.gb) return hipErrorInvalidValue;
   long blocks;
@@ -465,10 +492,8 @@ hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) {
   }
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_gemm3_big<EPI_STD>, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
-    (void)hipFuncSetAttribute((const void*)k_gemm3_big<EPI_EDGE>, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
-    (void)hipFuncSetAttribute((const void*)k_gemm3_big<EPI_SEGMEAN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kBigLds);
+    hipError_t e = gemm_init();
+    if (e != hipSuccess) return e;
     attr = true;
   }
   if (epi == EPI_EDGE)
@@ -490,7 +515,7 @@ static void launch3(const GemmArgs& g, int epi, long blocks, hipStream_t s) {
     hipLaunchKernelGGL((k_gemm3<EPI_STD, PF, REMAP>), dim3((unsigned)blocks), dim3(256), 0, s, g);
 }
 
-int g_gemm3_variant = 3;  // bit 0: two chunks in flight, bit 1: XCD remap
+int g_gemm3_variant = 0;  // bit 0: two chunks in flight, bit 1: XCD remap (0 measured fastest for node GEMMs)
 
 hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.N % XBN || g.K % (2 * XBK) || !g.Wp3) return hipErrorInvalidValue;

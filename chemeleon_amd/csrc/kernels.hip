@@ -277,8 +277,9 @@ hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P,
   return hipGetLastError();
 }
 
-__global__ void k_cond_in(const float* __restrict__ temb, int tstride, const float* __restrict__ text0,
-                          const float* __restrict__ text1, int text_dim, float* __restrict__ cin, int B, int P) {
+__global__ void k_cond_in(const float* __restrict__ temb, int tstride, const int* __restrict__ d_t,
+                          const float* __restrict__ text0, const float* __restrict__ text1, int text_dim,
+                          float* __restrict__ cin, int B, int P) {
   const int width = TD + text_dim;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)P * B * width) return;
@@ -286,13 +287,20 @@ __global__ void k_cond_in(const float* __restrict__ temb, int tstride, const flo
   const int k = (int)(idx - r * width);
   const int c = (int)(r / B), gph = (int)(r % B);
   const float* text = c == 0 ? text0 : text1;
-  cin[idx] = k < TD ? temb[(long)gph * tstride + k] : text[(long)gph * text_dim + (k - TD)];
+  const float* te = d_t ? temb + (long)(*d_t) * TD : temb + (long)gph * tstride;
+  cin[idx] = k < TD ? te[k] : text[(long)gph * text_dim + (k - TD)];
 }
-hipError_t build_cond_in(const float* temb, int tstride, const float* text0, const float* text1, int text_dim, float* cin,
-                         int B, int P, hipStream_t s) {
+hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
+                         int text_dim, float* cin, int B, int P, hipStream_t s) {
   const long n = (long)P * B * (TD + text_dim);
-  hipLaunchKernelGGL(k_cond_in, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, temb, tstride, text0, text1,
+  hipLaunchKernelGGL(k_cond_in, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, temb, tstride, d_t, text0, text1,
                      text_dim, cin, B, P);
+  return hipGetLastError();
+}
+
+__global__ void k_decrement(int* d_t) { *d_t -= 1; }
+hipError_t decrement(int* d_t, hipStream_t s) {
+  hipLaunchKernelGGL(k_decrement, dim3(1), dim3(1), 0, s, d_t);
   return hipGetLastError();
 }
 
@@ -480,13 +488,15 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
 __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* __restrict__ L1, long ld,
                                               const float* __restrict__ L2, float w1, float w2,
                                               const int64_t* __restrict__ xt, const int64_t* __restrict__ tnode,
-                                              int t_const, const float* __restrict__ noise,
+                                              int t_const, const int* __restrict__ d_t,
+                                              const float* __restrict__ noise,
                                               const float* __restrict__ q1, const float* __restrict__ qm,
                                               int64_t* __restrict__ out, uint64_t seed, int64_t node_base) {
   __shared__ float sm_all[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float* sm = sm_all[wv];
   const float eps = 1.0e-6f;
+  if (d_t) t_const = *d_t;
   for (long i = (long)blockIdx.x * 4 + wv; i < N; i += (long)gridDim.x * 4) {
     const int t = tnode ? (int)tnode[i] : t_const;
     const int d0 = lane, d1 = lane + 64;
@@ -547,15 +557,15 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
 }
 
 hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits, const float* logits2, float w1,
-                       float w2, const int64_t* xt, const int64_t* tnode, int t_const, const float* noise,
-                       const float* q1, const float* qm, int64_t* out, uint64_t seed, int64_t node_base,
-                       hipStream_t s) {
+                       float w2, const int64_t* xt, const int64_t* tnode, int t_const, const int* d_t,
+                       const float* noise, const float* q1, const float* qm, int64_t* out, uint64_t seed,
+                       int64_t node_base, hipStream_t s) {
   if (A > 128 || A < 1) return hipErrorInvalidValue;
   long blocks = (N + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_d3pm, dim3((unsigned)blocks), dim3(256), 0, s, N, A, T, logits, ld_logits, logits2, w1, w2, xt,
-                     tnode, t_const, noise, q1, qm, out, seed, node_base);
+                     tnode, t_const, d_t, noise, q1, qm, out, seed, node_base);
   return hipGetLastError();
 }
 
@@ -567,6 +577,7 @@ __constant__ float c_lat_mask[9] = {1.f, 0.f, 1.f, 1.f, 1.f, 1.f, 0.f, 0.f, 1.f}
 
 __global__ void k_step_predictor(StepArgs a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.d_t) a.t = *a.d_t;
   const float* cf = a.coef + (long)a.t * 8;
   const long nx = a.N * 3;
   if (idx < nx) {
@@ -601,6 +612,7 @@ __global__ void k_step_predictor(StepArgs a) {
 __global__ void k_step_corrector(StepArgs a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.N * 3) return;
+  if (a.d_t) a.t = *a.d_t;
   const float* cf = a.coef + (long)a.t * 8;
   const long i = idx / 3;
   const int k = (int)(idx - i * 3);
@@ -621,7 +633,8 @@ hipError_t step_predictor(const StepArgs& a, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return d3pm_sample((int)a.N, a.A, a.T, a.HO, HEADS_N, a.HO + a.N * HEADS_N, a.cs_null, a.cs_cond, a.a, nullptr,
-                     a.t, a.t > 1 ? a.ra : nullptr, a.q_one_step, a.q_mats, a.a, a.seed, a.node_base, s);
+                     a.t, a.d_t, (a.d_t || a.t > 1) ? a.ra : nullptr, a.q_one_step, a.q_mats, a.a, a.seed,
+                     a.node_base, s);
 }
 
 hipError_t step_corrector(const StepArgs& a, hipStream_t s) {

@@ -96,6 +96,10 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   hipStream_t s = (hipStream_t)stream;
   const int A = dims->max_atoms, L = dims->num_layers, X = dims->text_dim;
   const int CIN = TD + X, W1K = 2 * H + 9 + FD;
+  {
+    hipError_t e0 = gemm_init();
+    if (e0 != hipSuccess) return fail(CHM_E_HIP, std::string("gemm_init: ") + hipGetErrorString(e0));
+  }
 
   // layout of the packed arena (each piece 256-byte aligned)
   size_t off = 0;
@@ -456,13 +460,14 @@ static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const v
 
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
-                       int tstride, const float* text0, const float* text1, int heads, hipStream_t s) {
+                       int tstride, const int* d_t, const float* text0, const float* text1, int heads,
+                       hipStream_t s) {
   const chm_model* m = b->m;
   const int L = m->d.num_layers, X = m->d.text_dim, B = b->B;
   const long N = b->N, E = b->E, R = (long)P * N;
   const int CIN = TD + X;
   ProfScope whole(CHM_K_DECODER, s);
-  HIPCHK(build_cond_in(temb, tstride, text0, text1, X, b->cin, B, P, s));
+  HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
   {
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
@@ -540,7 +545,7 @@ extern "C" int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* a, co
   const float* t0 = text;
   const float* t1 = text ? text + (size_t)b->B * X : nullptr;
   const int heads = ((types_out || coords_out) ? 1 : 0) | (lattice_out ? 2 : 0);
-  int rc = run_decoder(b, pairs, a, x, lat, temb, time_stride, t0, t1, heads, s);
+  int rc = run_decoder(b, pairs, a, x, lat, temb, time_stride, nullptr, t0, t1, heads, s);
   if (rc) return rc;
   const long R = (long)pairs * b->N;
   if (heads & 1) HIPCHK(split_heads(b->HO, R, b->m->d.max_atoms, types_out, coords_out, s));
@@ -550,34 +555,51 @@ extern "C" int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* a, co
   return CHM_OK;
 }
 
-extern "C" int chm_sample_step(chm_batch* b, const chm_schedule* sc, int t, float cond_scale, int64_t* d_a, float* d_x,
-                               float* d_l, const float* d_cond, const float* d_null, const float* ra, const float* rl,
-                               const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
-                               int64_t graph_base, void* stream) {
+static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, float cond_scale, int64_t* d_a,
+                       float* d_x, float* d_l, const float* d_cond, const float* d_null, const float* ra,
+                       const float* rl, const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
+                       int64_t graph_base, hipStream_t s) {
   if (!b || !sc) return fail(CHM_E_ARG, "batch / schedule is NULL");
   if (b->P < 2) return fail(CHM_E_ARG, "sampling needs a batch created with max_pairs = 2");
-  if (t < 1 || t > sc->T) return fail(CHM_E_ARG, "t out of range");
+  if (!d_t && (t < 1 || t > sc->T)) return fail(CHM_E_ARG, "t out of range");
   if (!d_a || !d_x || !d_l || !sc->d_coef || !sc->d_time_emb || !sc->d_q_one_step || !sc->d_q_mats)
     return fail(CHM_E_ARG, "NULL state or schedule table");
   if (b->m->d.text_dim > 0 && (!d_cond || !d_null)) return fail(CHM_E_ARG, "cond / null embeddings required");
   if (ra && !(rl && rx1 && rx2)) return fail(CHM_E_ARG, "host noise: all four tensors or none");
-  hipStream_t s = (hipStream_t)stream;
-  const float* temb = sc->d_time_emb + (size_t)t * TD;
-  int rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_cond, d_null, 3, s);
+  // time-embedding row: host t -> pointer offset; device t -> offset inside the kernel
+  const float* temb = d_t ? sc->d_time_emb : sc->d_time_emb + (size_t)t * TD;
+  int rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 3, s);
   if (rc) return rc;
   StepArgs sa;
   std::memset(&sa, 0, sizeof(sa));
-  sa.t = t; sa.T = sc->T; sa.A = b->m->d.max_atoms; sa.N = b->N; sa.B = b->B;
+  sa.t = t; sa.d_t = d_t; sa.T = sc->T; sa.A = b->m->d.max_atoms; sa.N = b->N; sa.B = b->B;
   sa.cs_null = (float)(1.0 - (double)cond_scale); sa.cs_cond = cond_scale;
   sa.coef = sc->d_coef; sa.q_one_step = sc->d_q_one_step; sa.q_mats = sc->d_q_mats;
   sa.HO = b->HO; sa.LAT = b->LAT; sa.a = d_a; sa.x = d_x; sa.l = d_l; sa.n2g = b->n2g;
   sa.ra = ra; sa.rl = rl; sa.rx1 = rx1; sa.rx2 = rx2;
   sa.seed = seed; sa.node_base = node_base; sa.graph_base = graph_base;
   HIPCHK(step_predictor(sa, s));
-  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_cond, d_null, 1, s);
+  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 1, s);
   if (rc) return rc;
   HIPCHK(step_corrector(sa, s));
+  if (d_t) HIPCHK(decrement(d_t, s));
   return CHM_OK;
+}
+
+extern "C" int chm_sample_step(chm_batch* b, const chm_schedule* sc, int t, float cond_scale, int64_t* d_a, float* d_x,
+                               float* d_l, const float* d_cond, const float* d_null, const float* ra, const float* rl,
+                               const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
+                               int64_t graph_base, void* stream) {
+  return sample_step(b, sc, t, nullptr, cond_scale, d_a, d_x, d_l, d_cond, d_null, ra, rl, rx1, rx2, seed, node_base,
+                     graph_base, (hipStream_t)stream);
+}
+
+extern "C" int chm_sample_step_dt(chm_batch* b, const chm_schedule* sc, int32_t* d_t, float cond_scale, int64_t* d_a,
+                                  float* d_x, float* d_l, const float* d_cond, const float* d_null, uint64_t seed,
+                                  int64_t node_base, int64_t graph_base, void* stream) {
+  if (!d_t) return fail(CHM_E_ARG, "d_t is NULL");
+  return sample_step(b, sc, 0, d_t, cond_scale, d_a, d_x, d_l, d_cond, d_null, nullptr, nullptr, nullptr, nullptr,
+                     seed, node_base, graph_base, (hipStream_t)stream);
 }
 
 extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, float* agg, void* stream) {
@@ -592,7 +614,8 @@ extern "C" int chm_d3pm_sample(int N, int A, int T, const float* logits, const i
   if (N < 0 || A < 1 || A > 128 || T < 1) return fail(CHM_E_ARG, "bad sizes");
   if (N == 0) return CHM_OK;
   if (!logits || !xt || !tn || !noise || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
-  HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, noise, q1, qm, out, 0, 0, (hipStream_t)stream));
+  HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, noise, q1, qm, out, 0, 0,
+                     (hipStream_t)stream));
   return CHM_OK;
 }
 

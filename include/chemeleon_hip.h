@@ -149,6 +149,14 @@ int chm_sample_step(chm_batch* b, const chm_schedule* sched, int t, float cond_s
                     const float* d_rand_l, const float* d_rand_x1, const float* d_rand_x2, uint64_t seed,
                     int64_t node_base, int64_t graph_base, void* stream);
 
+/* Graph-capturable form of chm_sample_step: t is read from device memory
+ * (*d_t, int32) and decremented by the step's last kernel, so one captured
+ * step (hipStreamBeginCapture ... hipGraphLaunch) replayed T times walks
+ * t = T .. 1. Noise comes from the counter-based Philox generator only. */
+int chm_sample_step_dt(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale, int64_t* d_a,
+                       float* d_x, float* d_l, const float* d_cond, const float* d_null, uint64_t seed,
+                       int64_t node_base, int64_t graph_base, void* stream);
+
 /* Standalone message-passing aggregation (scatter_mean of edge messages onto
  * their source node; chemeleon/utils/scatter.py:88-112 as called from
  * cspnet.py:155-160) over this batch's fc edge layout:

@@ -336,9 +336,7 @@ def reference_single_step(m, natoms, a, x, lat, t, noise_seed):
     return captured["s"]
 
 
-def gen_trajectory(chm, csp):
-    """C0: 4 x 6 atoms, T = 100, seed 42, full reference sampler."""
-    m, sd = build_reference_model(chm, csp, 100)
+def _run_reference_trajectory(m, T, every):
     from chemeleon.modules import schema
     states = []
     orig_get = schema.TrajectoryContainer.get_atoms
@@ -351,20 +349,39 @@ def gen_trajectory(chm, csp):
     schema.TrajectoryContainer.get_atoms = get_atoms
     try:
         torch.manual_seed(42)
-        gen = m._sample_generator([6] * 4, ["Li1 Mn1 O4"] * 4, 2.0, 1e-5)
         last = None
-        for last in gen:
+        for last in m._sample_generator([6] * 4, ["Li1 Mn1 O4"] * 4, 2.0, 1e-5):
             pass
     finally:
         schema.TrajectoryContainer.get_atoms = orig_get
-    a = torch.stack([s[0] for s in states])
-    x = torch.stack([s[1] for s in states])
-    lat = torch.stack([s[2] for s in states])
-    # G6: ase-sorted output ordering of the final structures
+    keep = list(range(len(states) - 1, -1, -every))[::-1]  # always includes the final state (t = 0)
+    a = torch.stack([states[k][0] for k in keep])
+    x = torch.stack([states[k][1] for k in keep])
+    lat = torch.stack([states[k][2] for k in keep])
+    return a, x, lat, keep, last
+
+
+def gen_trajectory(chm, csp, T=100, every=1):
+    """C0: 4 x 6 atoms, seed 42, full reference sampler (T = 100: every state;
+    T = 1000: every `every`-th state, final state included). For T = 1000 the
+    reference is also run single-threaded: its difference to the 8-thread run
+    is the reference's own fp32 reordering drift, stored for comparison."""
+    m, sd = build_reference_model(chm, csp, T)
+    a, x, lat, keep, last = _run_reference_trajectory(m, T, every)
     order_numbers = np.concatenate([at.numbers for at in last])
     order_scaled = np.concatenate([at.scaled for at in last])
-    save("trajectory_4x6_T100.npz", atom_types=a, frac=x, lattices=lat, final_sorted_numbers=order_numbers,
-         final_sorted_scaled=order_scaled, weights_crc=weights_crc(sd))
+    ts = np.array([T - 1 - k for k in keep])
+    extra = {}
+    if T >= 1000:
+        nt = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            a1, x1, lat1, _, _ = _run_reference_trajectory(m, T, every)
+        finally:
+            torch.set_num_threads(nt)
+        extra = dict(atom_types_1thread=a1, frac_1thread=x1, lattices_1thread=lat1, threads=np.int64(nt))
+    save(f"trajectory_4x6_T{T}.npz", atom_types=a, frac=x, lattices=lat, final_sorted_numbers=order_numbers,
+         final_sorted_scaled=order_scaled, weights_crc=weights_crc(sd), t=ts, **extra)
 
 
 if __name__ == "__main__":
@@ -384,3 +401,5 @@ if __name__ == "__main__":
         gen_single_steps(chm, csp)
     if "trajectory" in which:
         gen_trajectory(chm, csp)
+    if "trajectory1000" in which:
+        gen_trajectory(chm, csp, T=1000, every=10)
