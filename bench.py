@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-samples", type=int, default=8)
     p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
+                   "captured HIP graph of the reverse step")
     p.add_argument("--math", choices=["bf16x3", "f32"], default="bf16x3",
                    help="decoder GEMM arithmetic (both fp32-accurate; see include/chemeleon_hip.h)")
     return p.parse_args()
@@ -149,14 +151,17 @@ def main():
 
     model.decoder.set_math(args.math)
     it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
-                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0)
+                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
+                             graph=not args.no_graph)
     next(it)  # initial state
+    # per-kernel HIP-event instrumentation: enabled before the first step so that in graph mode the
+    # event pairs are captured into the step graph and re-recorded by every replay (the read-out
+    # below then covers the last timed step; in eager mode every warm-up and timed launch)
+    _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
+    _lib.check(_lib.load().chm_prof_enable(1), "prof_enable")
     for _ in range(args.warmup):
         next(it)
     torch.cuda.synchronize()
-
-    _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
-    _lib.check(_lib.load().chm_prof_enable(1), "prof_enable")
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -231,7 +236,8 @@ def main():
         "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
                    "n_samples": total, "n_atoms": args.n_atoms, "timesteps": T_STEPS,
-                   "parallelism": f"sample-sharded x{world}", "noise": "philox (device)"},
+                   "parallelism": f"sample-sharded x{world}", "noise": "philox (device)",
+                   "launch": "eager" if args.no_graph else "hip graph replay per step"},
         "roofline": {"bound": "mfma",
                      "kernel": ("edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), both conditionings"
                                 if math == "bf16x3" else "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"),

@@ -177,10 +177,15 @@ class Chemeleon(nn.Module):
                       cond_scale: float = 2.0, step_lr: float = 1e-5, *, noise: str = "torch", seed: int = 0,
                       text_embeds=None, null_text_embeds=None, clone: bool = True, t_stop: int = 0,
                       node_base: int = 0, graph_base: int = 0,
-                      init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Iterator[Tuple]:
+                      init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                      graph: bool = False) -> Iterator[Tuple]:
         """Reverse loop of chemeleon.py:305-467 yielding device tensors
         (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
-        starting with the pure-noise state at t = T."""
+        starting with the pure-noise state at t = T.
+
+        graph=True (noise="philox" only): one reverse step is captured once
+        as a HIP graph (chm_sample_step_dt reads t from device memory and
+        decrements it) and replayed for every timestep."""
         if isinstance(natoms, int):
             natoms = [natoms]
         natoms = [int(n) for n in natoms]
@@ -216,6 +221,25 @@ class Chemeleon(nn.Module):
         stream = _lib.stream_handle(dev)
         emit = (lambda *ts: tuple(t.clone() for t in ts)) if clone else (lambda *ts: ts)
         yield (T,) + emit(a, x, lat)
+        if graph:
+            if noise != "philox":
+                raise ValueError("graph=True needs noise='philox' (host noise cannot be replayed)")
+            d_t = torch.full((1,), T, dtype=torch.int32, device=dev)
+            hg = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(hg, stream=side):
+                    _lib.check(L.chm_sample_step_dt(batch.handle, sched, _lib.ptr(d_t), float(cond_scale),
+                                                    _lib.ptr(a), _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond),
+                                                    _lib.ptr(null), seed, node_base, graph_base,
+                                                    _lib.stream_handle(dev)), "chm_sample_step_dt")
+            torch.cuda.current_stream(dev).wait_stream(side)
+            d_t.fill_(T)
+            for t in range(T, t_stop, -1):
+                hg.replay()
+                yield (t - 1,) + emit(a, x, lat)
+            return
         for t in range(T, t_stop, -1):
             if noise == "torch" and t > 1:
                 ra = torch.rand((N, A)).to(dev, non_blocking=False)  # :400-404

@@ -300,6 +300,21 @@ def test_philox_shard_invariance(model100, cn):
         assert torch.equal(cat, full[k]), f"state {k} differs between 1 and 2 shards"
 
 
+def test_graph_replay_matches_eager(model100, cn):
+    """One captured reverse step replayed per timestep (device-side t) gives
+    bit-identical states to eager stepping."""
+    nat = [5, 9, 3, 12]
+    runs = []
+    for graph in (False, True):
+        states = list(model100.sample_states(nat, None, 2.0, 1e-5, noise="philox", seed=11, text_embeds=cn[0],
+                                             null_text_embeds=cn[1], clone=True, graph=graph, t_stop=80))
+        runs.append(states)
+    assert [s[0] for s in runs[0]] == [s[0] for s in runs[1]]
+    for se, sg in zip(*runs):
+        for k in (1, 2, 3):
+            assert torch.equal(se[k], sg[k]), f"t={se[0]} state {k}"
+
+
 def test_large_batch_step_is_finite(model1000, cn):
     """512 x 40 (BASELINE metric shape): one reverse step in perf mode."""
     nat = [40] * 512
