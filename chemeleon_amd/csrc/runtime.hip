@@ -395,6 +395,8 @@ struct ProfScope {
   int id; hipStream_t s; hipEvent_t b = nullptr;
   ProfScope(int id_, hipStream_t s_) : id(id_), s(s_) {
     if (!g_prof_on || g_pool_next + 2 > g_pool.size()) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;  // not in graphs
     hipEvent_t a = g_pool[g_pool_next++];
     b = g_pool[g_pool_next++];
     if (hipEventRecord(a, s) != hipSuccess) { b = nullptr; return; }

@@ -178,6 +178,8 @@ int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* st
  * the kernels below with HIP events on the launch stream (a pool of 8192
  * pairs; recording stops when it is exhausted). After synchronising the
  * device, chm_prof_read returns the launch count and summed duration.
+ * Launches made while the stream is being captured into a graph are not
+ * instrumented (time a graph by replaying it; time kernels eagerly).
  *   CHM_K_EDGE_FOURIER  edge layer 1 (Fourier projection + node terms + SiLU)
  *   CHM_K_EDGE_MESSAGE  edge layer 2 (message GEMM + SiLU)
  *   CHM_K_SEGMENT_MEAN  message-passing aggregation (scatter_mean)
