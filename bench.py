@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
                    "captured HIP graph of the reverse step")
-    p.add_argument("--math", choices=["bf16x3", "f32"], default="bf16x3",
+    p.add_argument("--math", choices=["split16", "bf16x3", "f32"], default="split16",
                    help="decoder GEMM arithmetic (both fp32-accurate; see include/chemeleon_hip.h)")
     return p.parse_args()
 
@@ -203,7 +203,9 @@ def main():
     seg_bytes = 2.0 * (E * H * 4 + N * H * 4)
     step_flops = 2 * decoder_pair_flops(natoms)
     math = model.decoder.get_math()
-    peak = BF16X3_PEAK_TFLOPS if math == "bf16x3" else MFMA_F32_PEAK_TFLOPS
+    # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
+    # = bf16 rate) / 3 products; f32 = the fp32 MFMA peak
+    peak = {"bf16x3": BF16X3_PEAK_TFLOPS, "split16": MFMA_BF16_PEAK_TFLOPS / 3}.get(math, MFMA_F32_PEAK_TFLOPS)
 
     # standalone message-passing aggregation kernel (chm_segment_mean) on the
     # bench batch's edge layout, [2, E, 512] fp32 messages (HIP events)
@@ -239,7 +241,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32" if math == "f32" else "f32 (bf16x3-split MFMA, fp32 accumulate)",
+        "dtype": {"f32": "f32", "bf16x3": "f32 (bf16x3-split MFMA, fp32 accumulate)",
+                  "split16": "f32 (fp16x2-split edge GEMMs / bf16x3 node GEMMs, fp32 accumulate)"}[math],
         "data": "synthetic (seeded random-init weights of the real architecture; seeded conditioning vectors)",
         "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
@@ -250,11 +253,12 @@ def main():
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
                      "kernel": ("edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), both conditionings"
-                                if math == "bf16x3" else "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"),
+                                if math != "f32" else "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"),
                      "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
                      "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": None,
-                     "peak_note": ("fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products" if math == "bf16x3"
-                                   else "fp32 MFMA dense peak"),
+                     "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
+                                   "split16": "fp32-equivalent flops; fp16 dense MFMA 2.5 PF / 3 products",
+                                   "f32": "fp32 MFMA dense peak"}[math],
                      "flops_per_launch": msg_flops, "launches": nmsg,
                      "avg_ms": ms_msg / nmsg if nmsg else None},
         "msgpass": {"bound": "hbm", "kernel": "k_segment_mean (standalone scatter_mean, chm_segment_mean)",
@@ -262,7 +266,7 @@ def main():
                     "frac": (seg_gbs / HBM_PEAK_GBS) if seg_gbs else None, "bytes_per_launch": seg_bytes,
                     "avg_ms": seg_ms,
                     "note": ("in the sampler the aggregation is fused into the message GEMM epilogue; this is the "
-                             "standalone kernel on the same [2,E,512] shape" if math == "bf16x3" else
+                             "standalone kernel on the same [2,E,512] shape" if math != "f32" else
                              "the kernel as launched by the sampler")},
         "path": {"tflops": step_flops / s_per_step / 1e12, "mfma_frac": step_flops / s_per_step / 1e12 / peak,
                  "math": math, "flops_per_step_per_gpu": step_flops,

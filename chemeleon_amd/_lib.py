@@ -113,7 +113,7 @@ def require_device(*tensors):
             raise RuntimeError("chemeleon_amd expects contiguous tensors")
 
 
-MATH_BF16X3, MATH_F32 = 0, 1
+MATH_BF16X3, MATH_F32, MATH_SPLIT16 = 0, 1, 2
 K_EDGE_FOURIER, K_EDGE_MESSAGE, K_SEGMENT_MEAN, K_DECODER = 0, 1, 2, 3
 
 

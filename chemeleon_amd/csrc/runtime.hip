@@ -35,9 +35,11 @@ static int fail(int code, const std::string& msg) {
 struct LayerW {
   const float *WAB, *Wcl, *b1, *D, *W2, *b2, *W3, *b3, *W4, *b4, *lw, *lb;
   const void *WAB3, *D3, *W23, *W33, *W43;  // bf16 hi/mid/lo planes of the GEMM weights
+  void *D2h, *W22h;                          // fp16 hi/lo planes of the edge-GEMM weights (row-scaled)
+  float *Dsc, *W2sc;                         // their per-row power-of-two scales
 };
 
-enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1 };
+enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1, MATH_SPLIT16 = 2 };
 constexpr long kTileRows = 256;  // rows of the edge-GEMM tiles (gemm_bf16x3_big)
 
 struct chm_model {
@@ -47,7 +49,8 @@ struct chm_model {
   const float *emb, *Wc, *bc, *Wp, *bp, *fw, *fb, *Whead, *bhead, *Wlat, *flw, *flb;
   const void *Wc3, *Wp3, *Whead3;
   void* mem3 = nullptr;  // bf16 planes arena
-  int math = MATH_BF16X3;
+  void* mem2 = nullptr;  // fp16 planes + scales arena
+  int math = MATH_SPLIT16;
   std::vector<LayerW> layers;
 };
 
@@ -64,12 +67,13 @@ struct chm_batch {
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
+  unsigned* rowmax;  // split16: per-row max |S| of edge layer 1's output, [P][E]
   std::vector<void*> allocs;
   size_t bytes = 0;
 };
 
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
-extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.2 (gfx950; bf16x3-split or f32 MFMA)"; }
+extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.3 (gfx950; split16 / bf16x3 / f32 MFMA)"; }
 
 extern "C" int chm_num_params(const chm_dims* d) { return d ? 7 + 10 * d->num_layers + 6 : 0; }
 
@@ -198,7 +202,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   // bf16x3 planes of every GEMM weight (fp32-accurate bf16 MFMA path)
   {
     const char* env = getenv("CHM_MATH");
-    m->math = (env && std::string(env) == "f32") ? MATH_F32 : MATH_BF16X3;
+    const std::string mode = env ? env : "";
+    m->math = mode == "f32" ? MATH_F32 : mode == "bf16x3" ? MATH_BF16X3 : MATH_SPLIT16;
     struct Job { const float* src; size_t n; const void** dst; };
     std::vector<Job> jobs;
     jobs.push_back({m->Wc, (size_t)2 * H * CIN, &m->Wc3});
@@ -230,11 +235,24 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       }
       p3 += (3 * j.n * 2 + 255) / 256 * 256;
     }
-    e2 = hipStreamSynchronize(s);
+    // fp16 hi/lo planes (+ row scales) of the two edge-GEMM weights of every layer
+    const size_t per_layer = (2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2 + 2 * H * 4 + 1023) / 1024 * 1024;
+    e2 = hipMalloc(&m->mem2, per_layer * L);
+    for (int l = 0; l < L && e2 == hipSuccess; ++l) {
+      char* q = (char*)m->mem2 + per_layer * l;
+      LayerW& w = m->layers[l];
+      w.D2h = q;
+      w.W22h = q + 2 * (size_t)H * FD * 2;
+      w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2);
+      w.W2sc = w.Dsc + H;
+      e2 = split_planes_h(w.D, H, FD, w.D2h, w.Dsc, s);
+      if (e2 == hipSuccess) e2 = split_planes_h(w.W2, H, H, w.W22h, w.W2sc, s);
+    }
+    if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
     if (e2 != hipSuccess) {
-      (void)hipFree(m->mem); (void)hipFree(m->mem3);
+      (void)hipFree(m->mem); (void)hipFree(m->mem3); (void)hipFree(m->mem2);
       delete m;
-      return fail(CHM_E_HIP, std::string("plane split sync: ") + hipGetErrorString(e2));
+      return fail(CHM_E_HIP, std::string("plane split: ") + hipGetErrorString(e2));
     }
   }
   *out = m;
@@ -243,7 +261,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
 
 extern "C" int chm_model_set_math(chm_model* m, int mode) {
   if (!m) return fail(CHM_E_ARG, "model is NULL");
-  if (mode != CHM_MATH_BF16X3 && mode != CHM_MATH_F32) return fail(CHM_E_ARG, "unknown math mode");
+  if (mode != CHM_MATH_BF16X3 && mode != CHM_MATH_F32 && mode != CHM_MATH_SPLIT16)
+    return fail(CHM_E_ARG, "unknown math mode");
   m->math = mode;
   return CHM_OK;
 }
@@ -254,6 +273,7 @@ extern "C" void chm_model_destroy(chm_model* m) {
   if (!m) return;
   (void)hipFree(m->mem);
   (void)hipFree(m->mem3);
+  (void)hipFree(m->mem2);
   delete m;
 }
 
@@ -348,6 +368,7 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->F = fl((size_t)E * FD);
   b->S = fl((size_t)P * E * H);
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
+  b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
   b->LAT = fl((size_t)P * B * 9);
@@ -453,9 +474,16 @@ static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* 
   return gemm_bf16x3(g, epi, s);
 }
 
-// the two edge GEMMs (M = E or P*E rows): 256x256 tiles in bf16x3 mode
-static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
+// the two edge GEMMs (M = E or P*E rows): 256x256 tiles; split16 mode uses the fp16 hi/lo
+// planes (W2h, wsc) with row-scaled activations, bf16x3 mode the bf16 planes (W3)
+static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, const void* W2h,
+                                const float* wsc, hipStream_t s) {
   if (b->math == MATH_F32) return gemm(g, epi, s);
+  if (b->math == MATH_SPLIT16) {
+    g.Wp3 = W2h;
+    g.wscale = wsc;
+    return gemm_fp16x2_big(g, epi, s);
+  }
   g.Wp3 = W3;
   return gemm_bf16x3_big(g, epi, s);
 }
@@ -495,8 +523,12 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
       GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
       g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
+      if (b->math == MATH_SPLIT16) {
+        g.crowmax = b->rowmax;
+        HIPCHK(hipMemsetAsync(b->rowmax, 0, (size_t)P * E * sizeof(unsigned), s));
+      }
       ProfScope ps(CHM_K_EDGE_FOURIER, s);
-      HIPCHK(run_edge_gemm(b, g, EPI_EDGE, w.D3, s));
+      HIPCHK(run_edge_gemm(b, g, EPI_EDGE, w.D3, w.D2h, w.Dsc, s));
     }
     if (b->math == MATH_F32) {
       {  // edge layer 2: M = SiLU(S W2^T + b2)
@@ -511,8 +543,9 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, nullptr, H);
       g.bias = w.b2; g.act = 1; g.tiles = b->tiles; g.ntiles = b->ntiles; g.node_estart = b->node_estart;
       g.natoms = b->natoms; g.n2g = b->n2g; g.agg = b->agg; g.nnodes = N; g.npairs = P; g.E = E;
+      if (b->math == MATH_SPLIT16) g.arowmax = b->rowmax;
       ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-      HIPCHK(run_edge_gemm(b, g, EPI_SEGMEAN, w.W23, s));
+      HIPCHK(run_edge_gemm(b, g, EPI_SEGMEAN, w.W23, w.W22h, w.W2sc, s));
     }
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);

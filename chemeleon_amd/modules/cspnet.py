@@ -191,14 +191,14 @@ class CSPNet(nn.Module):
         return self._hip
 
     def set_math(self, mode: str):
-        """'bf16x3' (default) or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h)."""
-        code = {"bf16x3": _lib.MATH_BF16X3, "f32": _lib.MATH_F32}[mode]
+        """'split16' (default), 'bf16x3' or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h)."""
+        code = {"bf16x3": _lib.MATH_BF16X3, "f32": _lib.MATH_F32, "split16": _lib.MATH_SPLIT16}[mode]
         m = self.hip_model()
         _lib.check(_lib.load().chm_model_set_math(m.handle, code), "chm_model_set_math")
         self._batches.clear()
 
     def get_math(self) -> str:
-        return {0: "bf16x3", 1: "f32"}[_lib.load().chm_model_get_math(self.hip_model().handle)]
+        return {0: "bf16x3", 1: "f32", 2: "split16"}[_lib.load().chm_model_get_math(self.hip_model().handle)]
 
     def hip_batch(self, natoms, max_pairs: int = 1) -> HipBatch:
         key = (tuple(int(n) for n in natoms), max_pairs)

@@ -78,16 +78,22 @@ int chm_model_create(const chm_dims* dims, const float* const* d_params, int n_p
                      chm_model** out);
 void chm_model_destroy(chm_model* m);
 
-/* Arithmetic of the decoder GEMMs (both fp32-accurate):
- *   CHM_MATH_BF16X3 (default): each fp32 operand split into three bf16 parts,
- *     six bf16 MFMA products per fp32 product, fp32 accumulation; the edge
- *     message GEMM is fused with the scatter_mean aggregation.
+/* Arithmetic of the decoder GEMMs (all fp32-accurate, fp32 accumulation):
+ *   CHM_MATH_SPLIT16 (default): the two edge GEMMs split each operand into an
+ *     fp16 hi/lo pair (three fp16 MFMA products per fp32 product); W rows and
+ *     activation rows carry power-of-two scales so every split operand is
+ *     <= 1 in magnitude (the Fourier features already are; edge layer 1
+ *     records max|S| per row for edge layer 2). Node GEMMs use bf16x3.
+ *   CHM_MATH_BF16X3: every GEMM splits each operand into three bf16 parts,
+ *     six bf16 MFMA products per fp32 product.
  *   CHM_MATH_F32: v_mfma_f32_32x32x2_f32 (exact fp32 fma chains); standalone
  *     aggregation kernel.
- * The environment variable CHM_MATH=f32 selects the latter at creation.
- * A batch keeps the mode its model had when the batch was created. */
+ * In the two split modes the edge message GEMM is fused with scatter_mean.
+ * CHM_MATH=f32 / bf16x3 / split16 in the environment selects the mode at
+ * creation. A batch keeps the mode its model had when the batch was created. */
 #define CHM_MATH_BF16X3 0
 #define CHM_MATH_F32 1
+#define CHM_MATH_SPLIT16 2
 int chm_model_set_math(chm_model* m, int mode);
 int chm_model_get_math(const chm_model* m);
 

@@ -24,12 +24,16 @@ pytestmark = [pytest.mark.gpu,
 DEV = "cuda"
 
 
-def close(gpu, ref, rtol=1e-4, what=""):
+def scaled_err(gpu, ref):
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     scale = max(np.sqrt(np.mean(ref ** 2)), 1e-12)
-    err = np.abs(gpu - ref) / np.maximum(np.abs(ref), scale)
-    assert np.isfinite(gpu).all(), f"{what}: non-finite output"
+    return np.abs(gpu - ref) / np.maximum(np.abs(ref), scale)
+
+
+def close(gpu, ref, rtol=1e-4, what=""):
+    err = scaled_err(gpu, ref)
+    assert np.isfinite(np.asarray(gpu, dtype=np.float64)).all(), f"{what}: non-finite output"
     assert err.max() <= rtol, f"{what}: max scaled error {err.max():.3e} > {rtol}"
     return err.max()
 
@@ -104,7 +108,7 @@ def test_d3pm_bit_exact(model100, golden):
 
 
 # --------------------------------------------------------------------------- decoder
-MATHS = ["bf16x3", "f32"]
+MATHS = ["split16", "bf16x3", "f32"]
 
 
 @pytest.mark.parametrize("math", MATHS)
@@ -249,25 +253,38 @@ def test_decoder_large_ragged_vs_oracle(model1000, cn):
             close(latt[c].cpu(), rl, what=f"{math} lattice c={c}")
 
 
-def test_bf16x3_matches_f32_path(model1000, cn):
-    """The two GEMM arithmetics agree to fp32 rounding level on 64 x 20."""
+@pytest.mark.parametrize("t", [500, 1000])
+def test_math_modes_agree(model1000, cn, t):
+    """The GEMM arithmetics agree to fp32 rounding level on 64 x 20, for the
+    CFG pair (P = 2) and for a single conditioning (P = 1)."""
     nat = [20] * 64
     B, N = len(nat), sum(nat)
     g = torch.Generator().manual_seed(23)
     a = torch.randint(0, 104, (N,), generator=g).to(DEV)
     x = torch.rand(N, 3, generator=g).to(DEV)
     lat = (torch.randn(B, 3, 3, generator=g) * 4).to(DEV)
-    te = model1000.time_embed(torch.full((B,), 500, dtype=torch.long)).to(DEV)
+    te = model1000.time_embed(torch.full((B,), t, dtype=torch.long)).to(DEV)
     nat_t = torch.tensor(nat).to(DEV)
-    outs = {}
+    n2g = torch.arange(B).repeat_interleave(nat_t.cpu()).to(DEV)
+    outs, single = {}, {}
     for math in MATHS:
         model1000.decoder.set_math(math)
         outs[math] = model1000.decoder.forward_cfg(a, x, lat, nat_t, te, cn[0].expand(B, -1).to(DEV),
                                                    cn[1].expand(B, -1).to(DEV), need_nodes=True)
-    for k, name in enumerate(["types", "lattice", "coords", "nodes"]):
-        err = close(outs["bf16x3"][k].cpu(), outs["f32"][k].cpu(), rtol=2e-5, what=name)
-        print(f"bf16x3 vs f32 {name}: max scaled err {err:.2e}")
-    model1000.decoder.set_math("bf16x3")
+        single[math] = model1000.decoder(a, x, lat, nat_t, n2g, t=te, text_embeds=cn[0].expand(B, -1).to(DEV))
+    model1000.decoder.set_math("split16")
+    errs = {}
+    for m in ("split16", "bf16x3"):
+        for k, name in enumerate(["types", "lattice", "coords", "nodes"]):
+            for c in range(2):
+                e = scaled_err(outs[m][k][c].cpu(), outs["f32"][k][c].cpu())
+                errs[(m, "pair", c, name)] = (e.max(), np.median(e))
+            e = scaled_err(single[m][k].cpu(), single["f32"][k].cpu())
+            errs[(m, "single", 0, name)] = (e.max(), np.median(e))
+    for key, (e, med) in errs.items():
+        print(f"t={t} {key}: scaled err vs f32 max {e:.2e} median {med:.2e}")
+    bad = {k: e for k, (e, med) in errs.items() if e > 2e-5}
+    assert not bad, f"math modes disagree: {bad}"
 
 
 def test_sample_api_returns_sorted_structures(model100, golden, cn):
