@@ -41,6 +41,33 @@ struct GemmArgs {
 
 enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 
+// split16 edge GEMMs (edge_gemm.hip): both operands split into fp16 hi/lo, stored per row as
+// [K/32][hi 32 | lo 32] (a 32-deep K-tile of a row = one 128-B line), three fp16 MFMA products,
+// staged by global_load_lds.
+struct EdgeArgs {
+  long M;
+  int N, K;
+  const void* A;                  // split rows [rows][K/32][2][32] fp16
+  const int* aexp;               // per A row: 4 packed int8 exponents of its 128-column chunks, or null
+  const void* W;                 // split rows [N][K/32][2][32], rows scaled by 1 / wscale
+  const float* wscale;
+  float* C; long ldc;            // EPI_STD output
+  // EPI_EDGE: S[c][e] = SiLU(acc + PQ[c][ei[e]][:H] + PQ[c][ej[e]][H:]) written as scaled fp16 planes
+  const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
+  void* S; int* sexp;            // S as split rows [P*E][H/32][2][32] + packed chunk exponents
+  // EPI_SEGMEAN: agg[c][node] = mean over the node's edges of SiLU(acc + bias)
+  const float* bias;
+  const int2* tiles; int ntiles;
+  const long* node_estart;
+  const int* natoms; const int* n2g;
+  float* agg;
+  int dbg;  // microbenchmark ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers
+};
+hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
+hipError_t edge_gemm_init();
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s);
+hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
+
 hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
 // fp32-accurate GEMM on bf16 MFMA: A split on the fly into hi/mid/lo bf16,
 // W pre-split; six products per fp32 product, fp32 accumulation.

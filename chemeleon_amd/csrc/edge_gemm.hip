@@ -1,0 +1,451 @@
+// The two edge GEMMs of a CSP layer in "split16" arithmetic (cspnet.py:134-150:
+// edge_mlp = Linear(1801, H) . SiLU . Linear(H, H) . SiLU over all n^2 edges).
+//
+// Both operands arrive pre-split into fp16 hi/lo planes, x = hi + lo, and a
+// product is rebuilt from three fp16 MFMA products (a_hi w_lo + a_lo w_hi +
+// a_hi w_hi, fp32 accumulation on v_mfma_f32_32x32x16_f16). Power-of-two
+// scales keep every split operand <= 1 in magnitude, so the dropped a_lo w_lo
+// term and the fp16 subnormal floor stay at fp32-rounding level:
+//   * W rows: wscale[n] (split_planes_h), undone in the epilogue;
+//   * edge layer 1's A = the Fourier features, |f| <= 1, unscaled;
+//   * edge layer 2's A = S, scaled per (row, 128-column chunk) by 2^-e with e
+//     from the chunk's max |S|. Edge layer 1's epilogue computes e and writes
+//     S directly as scaled hi/lo planes; edge layer 2 rescales its fp32
+//     accumulators by 2^(e_prev - e_next) at each chunk boundary (exact).
+//
+// Because no operand needs converting on the way in, all four planes are staged
+// global -> LDS with global_load_lds (no VGPR round trip): a 4-deep LDS ring of
+// K-tiles of 16 (32 KB each), counted vmcnt waits and one raw barrier per tile
+// (cdna_hip_programming.md §5 'Pipelining across barriers'). 256x256 output
+// tiles, 8 waves of 64x128; accumulators are C^T fragments (the W fragment is
+// the MFMA A operand), so a lane owns an output row and float4 column groups.
+//
+// LDS image per plane and stage: [256 rows][16 fp16] = 32 B rows, the two 16-B
+// k-halves of row r stored swapped when (r >> 3) & 1 (the glds source address is
+// permuted, the LDS destination stays lane-linear), which makes the fragment
+// reads (lanes 0-15 = rows 0-15, one k-half) cover all 64 banks.
+#include "chm_internal.h"
+
+namespace chm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 32, NST = 2;
+constexpr int ROW_B = BK * 2 * 2;           // one row of a K-tile: 32 hi + 32 lo fp16 = one 128-B line
+constexpr int OPND_B = BM * ROW_B;          // 32 KB per operand per stage
+constexpr int STAGE_B = 2 * OPND_B;         // A, W
+constexpr int RING_B = NST * STAGE_B;       // 128 KB
+constexpr int SEG_TP = 132;                 // EPI_SEGMEAN column tile pitch (floats)
+constexpr int SEG_B = BM * SEG_TP * 4;      // 135168 B
+constexpr int LDS_B = RING_B > SEG_B ? RING_B : SEG_B;
+constexpr int CHUNK = 128;                  // S scale granularity (columns)
+
+__device__ __forceinline__ float silu_e(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+
+__device__ __forceinline__ long remap(long b, long nb) {
+  const long q = nb / 8, r = nb % 8, xcd = b % 8, idx = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// exponent e with m = f 2^e, f in [0.5, 1) (0 for m == 0)
+__device__ __forceinline__ int exp_of(float m) {
+  int e = 0;
+  if (m > 0.f) frexpf(m, &e);
+  return e;
+}
+
+}  // namespace
+
+template <int EPI, bool ASC>
+__global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int ntn = g.N / BN;
+  const long bid = remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(bid % ntn) * BN;
+  long row0, nrows;
+  int seg_c = 0;
+  int2 seg = {0, 0};
+  if (EPI == EPI_SEGMEAN) {
+    const long rest = bid / ntn;
+    seg_c = (int)(rest % g.npairs);
+    seg = g.tiles[rest / g.npairs];
+    const long es0 = g.node_estart[seg.x];
+    const long es1 = (seg.y < g.nnodes) ? g.node_estart[seg.y] : g.E;
+    row0 = (long)seg_c * g.E + es0;
+    nrows = es1 - es0;
+  } else {
+    row0 = (bid / ntn) * BM;
+    nrows = g.M - row0 < BM ? g.M - row0 : BM;
+  }
+  const int K = g.K, nk = K / BK;
+
+  // ---- glds sources. Operand rows are stored [K/32][hi 32 | lo 32] (fp16): the K-tile of a row
+  // is one 128-B line. Wave w stages rows 32w..32w+31 of both operands, 8 rows per instruction;
+  // lane -> (row 32w + 8q + (lane >> 3), LDS chunk lane & 7) holding line chunk
+  // (lane & 7) ^ swz(row), swz(row) = (row >> 1) & 7.
+  const char* Ab = reinterpret_cast<const char*>(g.A);
+  const char* Wb = reinterpret_cast<const char*>(g.W);
+  const long rowB = (long)K * 4;  // bytes per operand row
+  const char* ga[4];
+  const char* gw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = wave * 32 + q * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    ga[q] = Ab + (row0 + (r < nrows ? r : nrows - 1)) * rowB + lc * 16;
+    gw[q] = Wb + (long)(n0 + r) * rowB + lc * 16;
+  }
+  char* dst = lds + wave * 32 * ROW_B;
+  auto issue = [&](int t) {
+    const long k0 = (long)(t < nk ? t : nk - 1) * ROW_B;  // past the end: re-read the last tile
+    char* d = dst + (t % NST) * STAGE_B;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(ga[q] + k0), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(gw[q] + k0), (lds_void*)(d + OPND_B + q * 8 * ROW_B), 16, 0, 0);
+  };
+
+  // ---- row exponents of the A chunks (edge layer 2)
+  int ex[2] = {0, 0};
+  if (ASC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long lr = wm * 64 + i * 32 + r32;
+      ex[i] = g.aexp[row0 + (lr < nrows ? lr : nrows - 1)];
+    }
+  }
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // fragment (plane p, k-step ks, k-half h) of row r: logical chunk c = 4p + 2ks + h at
+  // physical chunk c ^ swz(r); swz depends on r32 only (tile rows are multiples of 16 apart)
+  const int swz = (r32 >> 1) & 7;
+  const int fa = (wm * 64 + r32) * ROW_B;
+  const int fw = OPND_B + (wn * 128 + r32) * ROW_B;
+  f16x8 fa_[2][2][2], fw_[2][2][4];  // [set][plane][i / j]
+  auto read_frags = [&](int set, int t, int ks) {
+    const char* S = lds + (t % NST) * STAGE_B;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int ch = 16 * ((4 * p + 2 * ks + h) ^ swz);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa_[set][p][i] = *reinterpret_cast<const f16x8*>(S + fa + i * 32 * ROW_B + ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fw_[set][p][j] = *reinterpret_cast<const f16x8*>(S + fw + j * 32 * ROW_B + ch);
+    }
+  };
+  auto mfmas = [&](int set) {
+    __builtin_amdgcn_s_setprio(1);
+    // small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][1][j], fa_[set][0][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][0][j], fa_[set][1][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][0][j], fa_[set][0][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto rescale = [&](int t) {
+    if (ASC && t > 0 && (t * BK) % CHUNK == 0) {
+      const int c = (t * BK) / CHUNK;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ep = (int)(signed char)(ex[i] >> (8 * (c - 1)));
+        const int en = (int)(signed char)(ex[i] >> (8 * c));
+        const float f = ldexpf(1.0f, ep - en);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] *= f;
+      }
+    }
+  };
+
+  // two-stage ring, K-tile t in stage t & 1. Fragments are double-buffered per 16-deep
+  // k-step: the barrier that publishes tile t+1 (and frees stage t for tile t+2) sits between
+  // tile t's two MFMA groups, so LDS reads always run under MFMAs.
+  issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  issue(1);
+  read_frags(0, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): set 0 (read under the last MFMAs) is in
+    read_frags(1, t, 1);
+    rescale(t);
+    mfmas(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): this wave is done reading stage t
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's part of tile t+1 has landed
+    if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();   // everyone's has; stage t & 1 is free
+    asm volatile("" ::: "memory");
+    if (!(g.dbg & 1)) issue(t + 2);
+    read_frags(0, t + 1, 0);                           // past the end: reads the re-read tile
+    mfmas(1);
+  }
+  // drain the ring (the tail re-reads still land in LDS) before the epilogue reuses it
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- undo the scales: W rows (columns of the output) and the last A chunk
+  {
+    float rs[2] = {1.0f, 1.0f};
+    if (ASC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] *= sc[e] * rs[i];
+      }
+  }
+
+  // lane l owns output row wm*64 + i*32 + (l & 31) and, per 4-register group q,
+  // the four consecutive columns wn*128 + j*32 + 8q + 4h .. +3
+  if (EPI == EPI_SEGMEAN) {
+    // two passes of 128 columns: the wn-th half of the waves writes SiLU(acc + b2) to an
+    // LDS tile [256][132], then every thread sums node segments of one column in edge order
+    float* T = reinterpret_cast<float*>(lds);
+    const long es0 = g.node_estart[seg.x];
+    for (int half = 0; half < 2; ++half) {
+      if (wn == half) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int col = j * 32 + 8 * q + 4 * h;
+            const f32x4 b = *reinterpret_cast<const f32x4*>(g.bias + n0 + half * 128 + col);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int row = wm * 64 + i * 32 + r32;
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = silu_e(acc[i][j][4 * q + e] + b[e]);
+              *reinterpret_cast<f32x4*>(T + row * SEG_TP + col) = v;
+            }
+          }
+      }
+      __syncthreads();
+      const int col = tid & 127;
+      for (int nd = seg.x + (tid >> 7); nd < seg.y; nd += 4) {
+        const int n = g.natoms[g.n2g[nd]];
+        const int r0 = (int)(g.node_estart[nd] - es0);
+        float sacc = 0.f;
+        for (int j = 0; j < n; ++j) sacc += T[(r0 + j) * SEG_TP + col];
+        g.agg[((long)seg_c * g.nnodes + nd) * H + n0 + half * 128 + col] = sacc / (float)(n < 1 ? 1 : n);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+
+  if (EPI == EPI_STD && !g.C) return;  // (microbenchmark: main loop only)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 64 + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+    if (EPI == EPI_EDGE) {
+      // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
+      // 128-column chunk (this wave's columns), e from the chunk's max |S|
+      // S values go through a wave-private LDS tile [32 rows][132] (pitch 132: the 16 lanes of
+      // a ds_write_b128 cover all banks) so the chunk max is known before the split
+      const long ii = g.ei[row], jj = g.ej[row];
+      _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
+      float* V = reinterpret_cast<float*>(lds) + wave * (32 * SEG_TP) + r32 * SEG_TP;
+      for (int c = 0; c < g.npairs; ++c) {
+        const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int lc = j * 32 + 8 * q + 4 * h;
+            const int col = n0 + wn * 128 + lc;
+            const f32x4 p = *reinterpret_cast<const f32x4*>(Pc + ii * (2 * H) + col);
+            const f32x4 qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
+              mx = fmaxf(mx, fabsf(v[e]));
+            }
+            *reinterpret_cast<f32x4*>(V + lc) = v;
+            __builtin_amdgcn_sched_barrier(0);  // bound the PQ loads in flight (register pressure)
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // lanes h = 0, 1 share the row
+        const int ex2 = exp_of(mx);
+        const float sc = ldexpf(1.0f, -ex2);
+        const long orow = (long)c * g.E + row;
+        _Float16* srow = S0 + orow * (2 * H);  // [H/32][hi 32 | lo 32]
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int lc = j * 32 + 8 * q + 4 * h;
+            const int col = n0 + wn * 128 + lc;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(V + lc);
+            f16x4 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = v[e] * sc;
+              hv[e] = (_Float16)x;
+              lv[e] = (_Float16)(x - (float)hv[e]);
+            }
+            _Float16* d = srow + (col / 32) * 64 + (col % 32);
+            *reinterpret_cast<f16x4*>(d) = hv;
+            *reinterpret_cast<f16x4*>(d + 32) = lv;
+          }
+        if (h == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+        }
+    }
+  }
+}
+
+hipError_t edge_gemm_init() {
+  const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false>, (const void*)k_edge_gemm<EPI_EDGE, false>,
+                      (const void*)k_edge_gemm<EPI_SEGMEAN, true>, (const void*)k_edge_gemm<EPI_STD, true>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
+  if (g.N % BN || g.K % BK || !g.A || !g.W || !g.wscale) return hipErrorInvalidValue;
+  const bool asc = g.aexp != nullptr;
+  if (asc && (g.K % CHUNK || g.K / CHUNK > 4)) return hipErrorInvalidValue;
+  long blocks;
+  if (epi == EPI_SEGMEAN) {
+    if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc) return hipErrorInvalidValue;
+    blocks = (long)g.ntiles * g.npairs * (g.N / BN);
+  } else {
+    if (g.M <= 0) return hipErrorInvalidValue;
+    if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || asc)) return hipErrorInvalidValue;
+    blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
+  }
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = edge_gemm_init();
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const dim3 grid((unsigned)blocks), block(512);
+  if (epi == EPI_EDGE)
+    hipLaunchKernelGGL((k_edge_gemm<EPI_EDGE, false>), grid, block, LDS_B, s, g);
+  else if (epi == EPI_SEGMEAN)
+    hipLaunchKernelGGL((k_edge_gemm<EPI_SEGMEAN, true>), grid, block, LDS_B, s, g);
+  else if (asc)
+    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, true>), grid, block, LDS_B, s, g);
+  else
+    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false>), grid, block, LDS_B, s, g);
+  return hipGetLastError();
+}
+
+// Fourier features (cspnet.py:38-52 as k_fourier) written split, rows [768/32][hi 32 | lo 32].
+__global__ void k_fourier_h(const float* __restrict__ x, const int* __restrict__ ei, const int* __restrict__ ej,
+                            long E, _Float16* __restrict__ F) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= E * 3 * NF) return;
+  const long e = idx / (3 * NF);
+  const int r = (int)(idx - e * 3 * NF);
+  const int a = r / NF, k = r - a * NF;
+  // torch.remainder(d, 1.0): fmod, negatives shifted by +1 (k_fourier's rem1)
+  float d = fmodf(__fsub_rn(x[(long)ej[e] * 3 + a], x[(long)ei[e] * 3 + a]), 1.0f);
+  if (d < 0.0f) d = __fadd_rn(d, 1.0f);
+  const float arg = __fmul_rn(d, __fmul_rn(6.28318548202514648f, (float)k));
+  const float sv = sinf(arg), cv = cosf(arg);
+  _Float16* f = F + e * (2 * FD);  // row layout [FD/32][hi 32 | lo 32]
+  const _Float16 sh = (_Float16)sv, ch = (_Float16)cv;
+  const int rs = (r / 32) * 64 + r % 32, rc = ((3 * NF + r) / 32) * 64 + r % 32;
+  f[rs] = sh;
+  f[rs + 32] = (_Float16)(sv - (float)sh);
+  f[rc] = ch;
+  f[rc + 32] = (_Float16)(cv - (float)ch);
+}
+
+// W [N][K] -> split rows [N][K/32][hi 32 | lo 32] of W * 2^-e_n, e_n the exponent of
+// max_k |W[n][k]| (every scaled entry <= 1), and wscale[n] = 2^e_n. One block per row.
+__global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ W, int K, _Float16* __restrict__ out,
+                                                      float* __restrict__ wscale) {
+  __shared__ float red[4];
+  const int n = blockIdx.x;
+  const float* row = W + (long)n * K;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) m = fmaxf(m, fabsf(row[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = exp_of(m);
+  const float sc = ldexpf(1.0f, -e);
+  _Float16* o = out + (long)n * 2 * K;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float x = row[k] * sc;
+    const _Float16 hi = (_Float16)x;
+    o[(k / 32) * 64 + k % 32] = hi;
+    o[(k / 32) * 64 + 32 + k % 32] = (_Float16)(x - (float)hi);
+  }
+  if (threadIdx.x == 0) wscale[n] = ldexpf(1.0f, e);
+}
+
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s) {
+  if (K % 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_split_rows_h, dim3(N), dim3(256), 0, s, W, K, reinterpret_cast<_Float16*>(out), wscale);
+  return hipGetLastError();
+}
+
+hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s) {
+  const long n = E * 3 * NF;
+  hipLaunchKernelGGL(k_fourier_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ei, ej, E,
+                     reinterpret_cast<_Float16*>(F));
+  return hipGetLastError();
+}
+
+}  // namespace chm

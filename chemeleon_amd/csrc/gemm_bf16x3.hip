@@ -335,16 +335,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
     if (m > 0.f) frexpf(m, &e);
     sscale = ldexpf(1.0f, -e);
   }
-  f32x4 ra0, ra1;
-  u32x4 rw[NP];
-  auto gload = [&](int k0) {
+  // two register sets: the global loads of K-tile t+2 are issued while tile t is
+  // computed and tile t+1 is converted into LDS (two tiles of latency cover)
+  f32x4 ra0[2], ra1[2];
+  u32x4 rw[2][NP];
+  auto gload = [&](int set, int k0) {
     const float* src = k0 < g.ksplit ? pa + k0 : pb + k0;
-    ra0 = *reinterpret_cast<const f32x4*>(src);
-    ra1 = *reinterpret_cast<const f32x4*>(src + 4);
+    ra0[set] = *reinterpret_cast<const f32x4*>(src);
+    ra1[set] = *reinterpret_cast<const f32x4*>(src + 4);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) rw[p] = *reinterpret_cast<const u32x4*>(pw + p * wplane + k0);
+    for (int p = 0; p < NP; ++p) rw[set][p] = *reinterpret_cast<const u32x4*>(pw + p * wplane + k0);
   };
-  auto lstore = [&](int st) {
+  auto lstore = [&](int set, int st) {
     __bf16* S = lsm + st * 2 * NP * LPLANE;
     const int off = srow * XLP + 8 * shalf;
     if (AR == 0) {
@@ -352,9 +354,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         __bf16 a, b, c;
-        split3(ra0[e], a, b, c);
+        split3(ra0[set][e], a, b, c);
         hh[e] = a; mm[e] = b; ll[e] = c;
-        split3(ra1[e], a, b, c);
+        split3(ra1[set][e], a, b, c);
         hh[4 + e] = a; mm[4 + e] = b; ll[4 + e] = c;
       }
       *reinterpret_cast<bf16x8*>(S + 0 * LPLANE + off) = hh;
@@ -365,16 +367,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         _Float16 x0, x1;
-        split2h(ra0[e] * sscale, x0, x1);
+        split2h(ra0[set][e] * sscale, x0, x1);
         hh[e] = x0; ll[e] = x1;
-        split2h(ra1[e] * sscale, x0, x1);
+        split2h(ra1[set][e] * sscale, x0, x1);
         hh[4 + e] = x0; ll[4 + e] = x1;
       }
       *reinterpret_cast<f16x8*>(S + 0 * LPLANE + off) = hh;
       *reinterpret_cast<f16x8*>(S + 1 * LPLANE + off) = ll;
     }
 #pragma unroll
-    for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(S + (NP + p) * LPLANE + off) = rw[p];
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(S + (NP + p) * LPLANE + off) = rw[set][p];
   };
 
   const int h = lane >> 5, r32 = lane & 31;
@@ -430,15 +432,25 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
   };
 
   const int nk = g.K / XBK;
-  gload(0);
-  lstore(0);
+  // loads and stores are unconditional (past the end they re-read the last K-tile and
+  // fill the idle stage) so the compiler can keep counted vmcnt waits across the loop
+  const int klast = (nk - 1) * XBK;
+  gload(0, 0);
+  gload(1, XBK < klast ? XBK : klast);
+  lstore(0, 0);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * XBK);
-    compute(st);
-    if (kt + 1 < nk) lstore(st ^ 1);
+  // tile t lives in register set t & 1 and LDS stage t & 1 (the set index must be a
+  // compile-time constant, hence the two-step body)
+  auto step = [&](int kt, int par) {
+    const int kn = (kt + 2) * XBK;
+    gload(par, kn < klast ? kn : klast);
+    compute(par);
+    lstore(par ^ 1, par ^ 1);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, 0);
+    if (kt + 1 < nk) step(kt + 1, 1);
   }
 
   // lane l owns output row wm*64 + i*32 + (l & 31) and, per 4-register group q,

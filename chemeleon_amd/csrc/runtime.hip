@@ -67,7 +67,7 @@ struct chm_batch {
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
-  unsigned* rowmax;  // split16: per-row max |S| of edge layer 1's output, [P][E]
+  unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
   std::vector<void*> allocs;
   size_t bytes = 0;
 };
@@ -102,6 +102,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   const int CIN = TD + X, W1K = 2 * H + 9 + FD;
   {
     hipError_t e0 = gemm_init();
+    if (e0 == hipSuccess) e0 = edge_gemm_init();
     if (e0 != hipSuccess) return fail(CHM_E_HIP, std::string("gemm_init: ") + hipGetErrorString(e0));
   }
 
@@ -245,8 +246,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       w.W22h = q + 2 * (size_t)H * FD * 2;
       w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2);
       w.W2sc = w.Dsc + H;
-      e2 = split_planes_h(w.D, H, FD, w.D2h, w.Dsc, s);
-      if (e2 == hipSuccess) e2 = split_planes_h(w.W2, H, H, w.W22h, w.W2sc, s);
+      e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, s);
+      if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, s);
     }
     if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
     if (e2 != hipSuccess) {
@@ -474,16 +475,9 @@ static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* 
   return gemm_bf16x3(g, epi, s);
 }
 
-// the two edge GEMMs (M = E or P*E rows): 256x256 tiles; split16 mode uses the fp16 hi/lo
-// planes (W2h, wsc) with row-scaled activations, bf16x3 mode the bf16 planes (W3)
-static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, const void* W2h,
-                                const float* wsc, hipStream_t s) {
+// the two edge GEMMs (M = E or P*E rows) in f32 / bf16x3 mode: 256x256 bf16x3 tiles
+static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
   if (b->math == MATH_F32) return gemm(g, epi, s);
-  if (b->math == MATH_SPLIT16) {
-    g.Wp3 = W2h;
-    g.wscale = wsc;
-    return gemm_fp16x2_big(g, epi, s);
-  }
   g.Wp3 = W3;
   return gemm_bf16x3_big(g, epi, s);
 }
@@ -504,7 +498,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
   HIPCHK(embed(a, m->emb, b->Hres, N, P, s));
-  HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
+  if (b->math == MATH_SPLIT16)
+    HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s));  // fp16 hi/lo planes [2][E][768] in F's bytes
+  else
+    HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
   for (int l = 0; l < L; ++l)
     HIPCHK(graph_bias(lat, m->layers[l].Wcl, 9, m->layers[l].b1, b->gbias + (size_t)l * B * H, B, s));
   for (int l = 0; l < L; ++l) {
@@ -520,32 +517,52 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
       HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s));
     }
-    {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
-      GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
-      g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
-      if (b->math == MATH_SPLIT16) {
-        g.crowmax = b->rowmax;
-        HIPCHK(hipMemsetAsync(b->rowmax, 0, (size_t)P * E * sizeof(unsigned), s));
+    if (b->math == MATH_SPLIT16) {
+      // split16: fp16 hi/lo split rows throughout (edge_gemm.hip). S lives in S's bytes as
+      // split rows [P*E][H/32][2][32] plus one packed exponent word per row (rowmax buffer).
+      int* sexp = reinterpret_cast<int*>(b->rowmax);
+      {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
+        EdgeArgs ea;
+        std::memset(&ea, 0, sizeof(ea));
+        ea.M = E; ea.N = H; ea.K = FD; ea.A = b->F; ea.W = w.D2h; ea.wscale = w.Dsc;
+        ea.ei = b->ei; ea.ej = b->ej; ea.PQ = b->PQ; ea.nnodes = N; ea.npairs = P; ea.E = E;
+        ea.S = b->S; ea.sexp = sexp;
+        ProfScope ps(CHM_K_EDGE_FOURIER, s);
+        HIPCHK(edge_gemm(ea, EPI_EDGE, s));
       }
-      ProfScope ps(CHM_K_EDGE_FOURIER, s);
-      HIPCHK(run_edge_gemm(b, g, EPI_EDGE, w.D3, w.D2h, w.Dsc, s));
-    }
-    if (b->math == MATH_F32) {
-      {  // edge layer 2: M = SiLU(S W2^T + b2)
-        GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
-        g.bias = w.b2; g.act = 1;
+      {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
+        EdgeArgs ea;
+        std::memset(&ea, 0, sizeof(ea));
+        ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
+        ea.W = w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles; ea.ntiles = b->ntiles;
+        ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
+        ea.nnodes = N; ea.npairs = P; ea.E = E;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-        HIPCHK(gemm(g, EPI_STD, s));
+        HIPCHK(edge_gemm(ea, EPI_SEGMEAN, s));
       }
-      ProfScope ps(CHM_K_SEGMENT_MEAN, s);
-      HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
-    } else {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2), M never stored
-      GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, nullptr, H);
-      g.bias = w.b2; g.act = 1; g.tiles = b->tiles; g.ntiles = b->ntiles; g.node_estart = b->node_estart;
-      g.natoms = b->natoms; g.n2g = b->n2g; g.agg = b->agg; g.nnodes = N; g.npairs = P; g.E = E;
-      if (b->math == MATH_SPLIT16) g.arowmax = b->rowmax;
-      ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-      HIPCHK(run_edge_gemm(b, g, EPI_SEGMEAN, w.W23, w.W22h, w.W2sc, s));
+    } else {
+      {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
+        GemmArgs g = gargs(E, H, FD, b->F, FD, w.D, b->S, H);
+        g.ei = b->ei; g.ej = b->ej; g.PQ = b->PQ; g.nnodes = N; g.npairs = P; g.E = E;
+        ProfScope ps(CHM_K_EDGE_FOURIER, s);
+        HIPCHK(run_edge_gemm(b, g, EPI_EDGE, w.D3, s));
+      }
+      if (b->math == MATH_F32) {
+        {  // edge layer 2: M = SiLU(S W2^T + b2)
+          GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, b->M, H);
+          g.bias = w.b2; g.act = 1;
+          ProfScope ps(CHM_K_EDGE_MESSAGE, s);
+          HIPCHK(gemm(g, EPI_STD, s));
+        }
+        ProfScope ps(CHM_K_SEGMENT_MEAN, s);
+        HIPCHK(segment_mean(b->M, b->agg, b->n2g, b->node_off, b->edge_off, b->natoms, N, E, P, s));
+      } else {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2), M never stored
+        GemmArgs g = gargs((long)P * E, H, H, b->S, H, w.W2, nullptr, H);
+        g.bias = w.b2; g.act = 1; g.tiles = b->tiles; g.ntiles = b->ntiles; g.node_estart = b->node_estart;
+        g.natoms = b->natoms; g.n2g = b->n2g; g.agg = b->agg; g.nnodes = N; g.npairs = P; g.E = E;
+        ProfScope ps(CHM_K_EDGE_MESSAGE, s);
+        HIPCHK(run_edge_gemm(b, g, EPI_SEGMEAN, w.W23, s));
+      }
     }
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);

@@ -8,6 +8,7 @@
 #include <vector>
 #include <functional>
 #include <cmath>
+#include <string>
 
 #include "../chemeleon_amd/csrc/chm_internal.h"
 
@@ -21,6 +22,15 @@ using namespace chm;
       exit(1);                                                                 \
     }                                                                          \
   } while (0)
+
+__global__ void split_h(const float* x, long n, _Float16* out) {  // split rows [..][K/32][2][32]
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const _Float16 h = (_Float16)x[i];
+  const long o = (i / 32) * 64 + i % 32;
+  out[o] = h;
+  out[o + 32] = (_Float16)(x[i] - (float)h);
+}
 
 __global__ void fill(float* p, long n, unsigned seed, float scale) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -60,6 +70,63 @@ int main(int argc, char** argv) {
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.A2 = A; g.lda2 = K; g.ksplit = K;
   g.W = W; g.ldw = K; g.C = C; g.ldc = N; g.bias = bias; g.act = 1; g.gb_rowmod = 1; g.Wp3 = W3;
   const double flops = 2.0 * M * N * K;
+  if (argc > 3 && std::string(argv[3]) == "edge") {  // glds edge GEMM only (PMC runs); "edge0" = no C stores
+    void* W2h; float* wsc; _Float16* Ah;
+    CK(hipMalloc(&W2h, 2L * N * K * 2)); CK(hipMalloc(&wsc, N * 4)); CK(hipMalloc(&Ah, 2L * M * K * 2));
+    CK(split_rows_h(W, N, K, W2h, wsc, s));
+    split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
+    EdgeArgs ea{};
+    ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2h; ea.wscale = wsc; ea.C = C; ea.ldc = N;
+    float te = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    ea.C = nullptr;
+    float t0 = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    printf("M=%ld K=%d glds edge GEMM: %.3f ms %.1f TF fp32-eq; without C stores %.3f ms %.1f TF\n", M, K, te,
+           flops / te / 1e9, t0, flops / t0 / 1e9);
+    for (int dbg = 1; dbg < 4; ++dbg) {
+      ea.dbg = dbg;
+      float td = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+      printf("  ablation %d (%s%s): %.3f ms %.1f TF\n", dbg, dbg & 1 ? "no loop loads " : "", dbg & 2 ? "no barriers" : "",
+             td, flops / td / 1e9);
+    }
+    ea.dbg = 0;
+    return 0;
+  }
+  if (argc > 3 && std::string(argv[3]) == "f16") {  // fp16x2 big only (PMC runs)
+    void* W2h; float* wsc;
+    CK(hipMalloc(&W2h, 2L * N * K * 2)); CK(hipMalloc(&wsc, N * 4));
+    CK(split_planes_h(W, N, K, W2h, wsc, s));
+    GemmArgs gh = g; gh.Wp3 = W2h; gh.wscale = wsc;
+    float th = time_it(5, s, [&] { CK(gemm_fp16x2_big(gh, EPI_STD, s)); });
+    printf("M=%ld N=%d K=%d fp16x2 big (3 products): %.3f ms %.1f TF fp32-equivalent\n", M, N, K, th, flops / th / 1e9);
+    // glds edge GEMM on pre-split rows
+    _Float16* Ah; int* aexp; void* W2r;
+    CK(hipMalloc(&Ah, 2L * M * K * 2)); CK(hipMalloc(&aexp, M * 4)); CK(hipMemset(aexp, 0, M * 4));
+    CK(hipMalloc(&W2r, 2L * N * K * 2));
+    CK(split_rows_h(W, N, K, W2r, wsc, s));
+    split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
+    EdgeArgs ea{};
+    ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2r; ea.wscale = wsc; ea.C = C; ea.ldc = N;
+    float te = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    printf("  glds edge GEMM: %.3f ms %.1f TF fp32-equivalent\n", te, flops / te / 1e9);
+    std::vector<float> c1(65536 * 4), c2(65536 * 4);
+    GemmArgs gp = g; gp.bias = nullptr; gp.act = 0;
+    CK(gemm(gp, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
+    CK(edge_gemm(ea, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0, ref = 0;
+    for (size_t i = 0; i < c1.size(); ++i) { mx = fmax(mx, fabs((double)c1[i] - c2[i])); ref = fmax(ref, fabs((double)c1[i])); }
+    printf("  max |edge - f32mfma| = %.3e (max |C| %.3e)\n", mx, ref);
+    if (K % 128 == 0 && K <= 512) {
+      ea.aexp = aexp;
+      float ta = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+      CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
+      mx = 0;
+      for (size_t i = 0; i < c1.size(); ++i) mx = fmax(mx, fabs((double)c1[i] - c2[i]));
+      printf("  glds edge GEMM, chunk-scaled A: %.3f ms %.1f TF, max err %.3e\n", ta, flops / ta / 1e9, mx);
+    }
+    return 0;
+  }
   float t32 = time_it(5, s, [&] { CK(gemm(g, EPI_STD, s)); });
   printf("M=%ld N=%d K=%d  f32-mfma: %.3f ms %.1f TF\n", M, N, K, t32, flops / t32 / 1e9);
   for (int v = 0; v < 4; ++v) {
