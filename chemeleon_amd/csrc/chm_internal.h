@@ -54,7 +54,8 @@ struct EdgeArgs {
   float* C; long ldc;            // EPI_STD output
   // EPI_EDGE: S[c][e] = SiLU(acc + PQ[c][ei[e]][:H] + PQ[c][ej[e]][H:]) written as scaled fp16 planes
   const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
-  void* S; int* sexp;            // S as split rows [P*E][H/32][2][32] + packed chunk exponents
+  void* S; int* sexp;            // S as split rows [P*E][H/32][2][32] (columns permuted within each
+                                 // 32-chunk, see edge_gemm.hip) + packed chunk exponents
   // EPI_SEGMEAN: agg[c][node] = mean over the node's edges of SiLU(acc + bias)
   const float* bias;
   const int2* tiles; int ntiles;
@@ -65,7 +66,7 @@ struct EdgeArgs {
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
-hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s);
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
 
 hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);

@@ -311,24 +311,29 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
         const float sc = ldexpf(1.0f, -ex2);
         const long orow = (long)c * g.E + row;
         _Float16* srow = S0 + orow * (2 * H);  // [H/32][hi 32 | lo 32]
+        // S is stored with the columns of each 32-chunk permuted, 8q + 4h + e -> 16h + 4q + e
+        // (W2's K index carries the same permutation, split_rows_h(perm)), so a lane's 16 values
+        // of a chunk are contiguous: two 16-B stores per plane
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          f16x8 hv[2], lv[2];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int lc = j * 32 + 8 * q + 4 * h;
-            const int col = n0 + wn * 128 + lc;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(V + lc);
-            f16x4 hv, lv;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(V + j * 32 + 8 * q + 4 * h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float x = v[e] * sc;
-              hv[e] = (_Float16)x;
-              lv[e] = (_Float16)(x - (float)hv[e]);
+              const _Float16 hx = (_Float16)x;
+              hv[q >> 1][4 * (q & 1) + e] = hx;
+              lv[q >> 1][4 * (q & 1) + e] = (_Float16)(x - (float)hx);
             }
-            _Float16* d = srow + (col / 32) * 64 + (col % 32);
-            *reinterpret_cast<f16x4*>(d) = hv;
-            *reinterpret_cast<f16x4*>(d + 32) = lv;
           }
+          _Float16* d = srow + ((n0 + wn * 128) / 32 + j) * 64 + 16 * h;
+          *reinterpret_cast<f16x8*>(d) = hv[0];
+          *reinterpret_cast<f16x8*>(d + 8) = hv[1];
+          *reinterpret_cast<f16x8*>(d + 32) = lv[0];
+          *reinterpret_cast<f16x8*>(d + 40) = lv[1];
+        }
         if (h == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
       }
     } else {
@@ -411,8 +416,10 @@ __global__ void k_fourier_h(const float* __restrict__ x, const int* __restrict__
 
 // W [N][K] -> split rows [N][K/32][hi 32 | lo 32] of W * 2^-e_n, e_n the exponent of
 // max_k |W[n][k]| (every scaled entry <= 1), and wscale[n] = 2^e_n. One block per row.
+// perm: store column 8q + 4h + e of each 32-chunk at 16h + 4q + e (the layout edge layer 1's
+// epilogue writes S in; applied to W2's K index).
 __global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ W, int K, _Float16* __restrict__ out,
-                                                      float* __restrict__ wscale) {
+                                                      float* __restrict__ wscale, int perm) {
   __shared__ float red[4];
   const int n = blockIdx.x;
   const float* row = W + (long)n * K;
@@ -429,15 +436,16 @@ __global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ 
   for (int k = threadIdx.x; k < K; k += 256) {
     const float x = row[k] * sc;
     const _Float16 hi = (_Float16)x;
-    o[(k / 32) * 64 + k % 32] = hi;
-    o[(k / 32) * 64 + 32 + k % 32] = (_Float16)(x - (float)hi);
+    const int c = k % 32, pc = perm ? 16 * ((c >> 2) & 1) + 4 * (c >> 3) + (c & 3) : c;
+    o[(k / 32) * 64 + pc] = hi;
+    o[(k / 32) * 64 + 32 + pc] = (_Float16)(x - (float)hi);
   }
   if (threadIdx.x == 0) wscale[n] = ldexpf(1.0f, e);
 }
 
-hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s) {
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s) {
   if (K % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_split_rows_h, dim3(N), dim3(256), 0, s, W, K, reinterpret_cast<_Float16*>(out), wscale);
+  hipLaunchKernelGGL(k_split_rows_h, dim3(N), dim3(256), 0, s, W, K, reinterpret_cast<_Float16*>(out), wscale, perm);
   return hipGetLastError();
 }
 

@@ -246,8 +246,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       w.W22h = q + 2 * (size_t)H * FD * 2;
       w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2);
       w.W2sc = w.Dsc + H;
-      e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, s);
-      if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, s);
+      e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, 0, s);
+      if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, 1, s);  // K permuted like S
     }
     if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
     if (e2 != hipSuccess) {

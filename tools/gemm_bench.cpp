@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
   if (argc > 3 && std::string(argv[3]) == "edge") {  // glds edge GEMM only (PMC runs); "edge0" = no C stores
     void* W2h; float* wsc; _Float16* Ah;
     CK(hipMalloc(&W2h, 2L * N * K * 2)); CK(hipMalloc(&wsc, N * 4)); CK(hipMalloc(&Ah, 2L * M * K * 2));
-    CK(split_rows_h(W, N, K, W2h, wsc, s));
+    CK(split_rows_h(W, N, K, W2h, wsc, 0, s));
     split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
     EdgeArgs ea{};
     ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2h; ea.wscale = wsc; ea.C = C; ea.ldc = N;
@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
     _Float16* Ah; int* aexp; void* W2r;
     CK(hipMalloc(&Ah, 2L * M * K * 2)); CK(hipMalloc(&aexp, M * 4)); CK(hipMemset(aexp, 0, M * 4));
     CK(hipMalloc(&W2r, 2L * N * K * 2));
-    CK(split_rows_h(W, N, K, W2r, wsc, s));
+    CK(split_rows_h(W, N, K, W2r, wsc, 0, s));
     split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
     EdgeArgs ea{};
     ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2r; ea.wscale = wsc; ea.C = C; ea.ldc = N;
