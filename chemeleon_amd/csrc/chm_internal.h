@@ -32,11 +32,6 @@ struct GemmArgs {
   const long* node_estart;                // first edge row of each node
   const int* natoms; const int* n2g;
   float* agg;                             // [P][N][H]
-  const float* wscale;                    // fp16x2: per-W-row power-of-two scale (undone in the epilogue)
-  // fp16x2 with row-scaled A: arowmax[r] = bits of max_k |A[r][k]| (A rows scaled by 2^-exponent
-  // before the split, undone in the epilogue). EPI_EDGE writes it for its output S (atomicMax).
-  const unsigned* arowmax;
-  unsigned* crowmax;
 };
 
 enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
@@ -62,7 +57,8 @@ struct EdgeArgs {
   const long* node_estart;
   const int* natoms; const int* n2g;
   float* agg;
-  int dbg;  // microbenchmark ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers
+  int dbg;  // profiling ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers,
+            // bit 2 = no epilogue stores (EDGE / SEGMEAN), bit 3 = no PQ loads (EDGE)
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
@@ -77,8 +73,6 @@ hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s);
 hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s);
 hipError_t gemm_init();  // one-time kernel attributes (call outside stream capture)
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
-hipError_t gemm_fp16x2_big(const GemmArgs& g, int epi, hipStream_t s);
-hipError_t split_planes_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s);
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
 

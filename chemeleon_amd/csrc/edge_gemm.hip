@@ -37,11 +37,12 @@ typedef const __attribute__((address_space(1))) void gbl_void;
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 32, NST = 2;
+constexpr int BM = 256, BN = 256, BK = 32;
+constexpr int NSA = 3, NSW = 2;             // ring depths: A (streamed from HBM) and W (L2-resident)
 constexpr int ROW_B = BK * 2 * 2;           // one row of a K-tile: 32 hi + 32 lo fp16 = one 128-B line
-constexpr int OPND_B = BM * ROW_B;          // 32 KB per operand per stage
-constexpr int STAGE_B = 2 * OPND_B;         // A, W
-constexpr int RING_B = NST * STAGE_B;       // 128 KB
+constexpr int OPND_B = BM * ROW_B;          // 32 KB per operand tile
+constexpr int W_RING = NSA * OPND_B;        // W stages follow the A stages
+constexpr int RING_B = (NSA + NSW) * OPND_B;  // 160 KB
 constexpr int SEG_TP = 132;                 // EPI_SEGMEAN column tile pitch (floats)
 constexpr int SEG_B = BM * SEG_TP * 4;      // 135168 B
 constexpr int LDS_B = RING_B > SEG_B ? RING_B : SEG_B;
@@ -98,25 +99,36 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   const char* Ab = reinterpret_cast<const char*>(g.A);
   const char* Wb = reinterpret_cast<const char*>(g.W);
   const long rowB = (long)K * 4;  // bytes per operand row
-  const char* ga[4];
-  const char* gw[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = wave * 32 + q * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ ((r >> 1) & 7);
-    ga[q] = Ab + (row0 + (r < nrows ? r : nrows - 1)) * rowB + lc * 16;
-    gw[q] = Wb + (long)(n0 + r) * rowB + lc * 16;
-  }
+  // uniform block bases + 32-bit per-lane offsets (keeps the address VGPRs few)
+  const char* Ablk = Ab + row0 * rowB;
+  const char* Wblk = Wb + (long)n0 * rowB;
+  const int lr0 = wave * 32 + (lane >> 3);
+  const unsigned lc16 = 16u * (unsigned)((lane & 7) ^ ((lr0 >> 1) & 7));  // (r >> 1) & 7 is the same for r + 8q
+  // (the per-row A offsets are recomputed at each issue: hoisted, they cost 4 VGPRs the
+  // main loop does not have)
+  int lr0v = lr0;
+  unsigned lcv = lc16;
+  const unsigned woff = (unsigned)(lr0 * rowB) + lc16;
+  const unsigned wq = (unsigned)(8 * rowB);
   char* dst = lds + wave * 32 * ROW_B;
-  auto issue = [&](int t) {
-    const long k0 = (long)(t < nk ? t : nk - 1) * ROW_B;  // past the end: re-read the last tile
-    char* d = dst + (t % NST) * STAGE_B;
+  // past the end of K the loads re-read the last tile into an idle stage
+  auto issueA = [&](int t) {
+    const char* src = Ablk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dst + (t % NSA) * OPND_B;
+    asm volatile("" : "+v"(lr0v), "+v"(lcv));  // keep the offsets from being hoisted
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = lr0v + q * 8;
+      const unsigned off = (unsigned)((r < nrows ? r : (int)nrows - 1) * (int)rowB) + lcv;
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + off), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
+    }
+  };
+  auto issueW = [&](int t) {
+    const char* src = Wblk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dst + W_RING + (t % NSW) * OPND_B;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(ga[q] + k0), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(gw[q] + k0), (lds_void*)(d + OPND_B + q * 8 * ROW_B), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq)), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
   };
 
   // ---- row exponents of the A chunks (edge layer 2)
@@ -141,17 +153,18 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   // physical chunk c ^ swz(r); swz depends on r32 only (tile rows are multiples of 16 apart)
   const int swz = (r32 >> 1) & 7;
   const int fa = (wm * 64 + r32) * ROW_B;
-  const int fw = OPND_B + (wn * 128 + r32) * ROW_B;
+  const int fw = (wn * 128 + r32) * ROW_B;
   f16x8 fa_[2][2][2], fw_[2][2][4];  // [set][plane][i / j]
   auto read_frags = [&](int set, int t, int ks) {
-    const char* S = lds + (t % NST) * STAGE_B;
+    const char* SA = lds + (t % NSA) * OPND_B;
+    const char* SW = lds + W_RING + (t % NSW) * OPND_B;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int ch = 16 * ((4 * p + 2 * ks + h) ^ swz);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa_[set][p][i] = *reinterpret_cast<const f16x8*>(S + fa + i * 32 * ROW_B + ch);
+      for (int i = 0; i < 2; ++i) fa_[set][p][i] = *reinterpret_cast<const f16x8*>(SA + fa + i * 32 * ROW_B + ch);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fw_[set][p][j] = *reinterpret_cast<const f16x8*>(S + fw + j * 32 * ROW_B + ch);
+      for (int j = 0; j < 4; ++j) fw_[set][p][j] = *reinterpret_cast<const f16x8*>(SW + fw + j * 32 * ROW_B + ch);
     }
   };
   auto mfmas = [&](int set) {
@@ -188,26 +201,34 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     }
   };
 
-  // two-stage ring, K-tile t in stage t & 1. Fragments are double-buffered per 16-deep
-  // k-step: the barrier that publishes tile t+1 (and frees stage t for tile t+2) sits between
-  // tile t's two MFMA groups, so LDS reads always run under MFMAs.
-  issue(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // rings: A tile t in A stage t % 3 (two tiles of HBM latency cover), W tile t in W stage t % 2.
+  // Fragments are double-buffered per 16-deep k-step: the barrier that publishes tile t+1 (and
+  // frees tile t's stages) sits between tile t's two MFMA groups, so LDS reads run under MFMAs.
+  // Issue order W0 A0 A1 W1 A2 | W2 A3 | W3 A4 ...: when tile t+1 is needed only A(t+2) may be
+  // outstanding, vmcnt(4).
+  issueW(0);
+  issueA(0);
+  issueA(1);
+  issueW(1);
+  issueA(2);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  issue(1);
   read_frags(0, 0, 0);
   for (int t = 0; t < nk; ++t) {
     __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): set 0 (read under the last MFMAs) is in
     read_frags(1, t, 1);
     rescale(t);
     mfmas(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): this wave is done reading stage t
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's part of tile t+1 has landed
-    if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();   // everyone's has; stage t & 1 is free
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // this wave is done reading tile t
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this thread's part of tile t+1 has landed
+    if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();   // everyone's has; tile t's stages are free
     asm volatile("" ::: "memory");
-    if (!(g.dbg & 1)) issue(t + 2);
-    read_frags(0, t + 1, 0);                           // past the end: reads the re-read tile
+    if (!(g.dbg & 1)) {
+      issueW(t + 2);
+      issueA(t + 3);
+    }
+    read_frags(0, t + 1, 0);                           // past the end: reads a re-read tile
     mfmas(1);
   }
   // drain the ring (the tail re-reads still land in LDS) before the epilogue reuses it
@@ -265,7 +286,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
         const int r0 = (int)(g.node_estart[nd] - es0);
         float sacc = 0.f;
         for (int j = 0; j < n; ++j) sacc += T[(r0 + j) * SEG_TP + col];
-        g.agg[((long)seg_c * g.nnodes + nd) * H + n0 + half * 128 + col] = sacc / (float)(n < 1 ? 1 : n);
+        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + nd) * H + n0 + half * 128 + col] = sacc / (float)(n < 1 ? 1 : n);
       }
       __syncthreads();
     }
@@ -295,8 +316,11 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
           for (int q = 0; q < 4; ++q) {
             const int lc = j * 32 + 8 * q + 4 * h;
             const int col = n0 + wn * 128 + lc;
-            const f32x4 p = *reinterpret_cast<const f32x4*>(Pc + ii * (2 * H) + col);
-            const f32x4 qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
+            f32x4 p = {0.f, 0.f, 0.f, 0.f}, qv = p;
+            if (!(g.dbg & 8)) {
+              p = *reinterpret_cast<const f32x4*>(Pc + ii * (2 * H) + col);
+              qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
+            }
             f32x4 v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -329,6 +353,10 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
             }
           }
           _Float16* d = srow + ((n0 + wn * 128) / 32 + j) * 64 + 16 * h;
+          if (g.dbg & 4) {  // profiling: keep the values live, store nothing
+            asm volatile("" ::"v"(hv[0]), "v"(hv[1]), "v"(lv[0]), "v"(lv[1]));
+            continue;
+          }
           *reinterpret_cast<f16x8*>(d) = hv[0];
           *reinterpret_cast<f16x8*>(d + 8) = hv[1];
           *reinterpret_cast<f16x8*>(d + 32) = lv[0];

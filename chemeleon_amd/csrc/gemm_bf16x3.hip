@@ -24,7 +24,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float silu3(float x) { return x / (1.0f + expf(-x)); }
 // epilogue SiLU: hardware exp2 + reciprocal (~2 ulp; the reference's own
@@ -51,12 +50,6 @@ __device__ __forceinline__ long xcd_remap(long b, long nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-// fp16 hi/lo split for |x| <= 1 operands: x = h + l + r, |r| <= 2^-23 |x| (plus the fp16
-// subnormal floor 2^-25 absolute)
-__device__ __forceinline__ void split2h(float x, _Float16& h, _Float16& l) {
-  h = (_Float16)x;
-  l = (_Float16)(x - (float)h);
-}
 
 template <int EPI, int PF, int REMAP>
 __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs g) {
@@ -282,12 +275,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs g) {
 constexpr int LBM = 256, LBN = 256;
 constexpr int LPLANE = 256 * XLP;
 
-// AR = 0: bf16x3 (three bf16 planes per operand, six products);
-// AR = 1: fp16x2 (two fp16 planes per operand, three products) for |A| <= 1 operands
-//         (the Fourier features); W rows carry a power-of-two scale undone in the epilogue.
-template <int EPI, int AR>
+template <int EPI>
 __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
-  constexpr int NP = AR ? 2 : 3;  // planes per operand
+  constexpr int NP = 3;  // planes per operand
   extern __shared__ __attribute__((aligned(16))) __bf16 lsm[];  // [2][2*NP][LPLANE]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -327,14 +317,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
   const float* pa = g.A + ar * g.lda + 8 * shalf;
   const float* pb = g.A2 + ar * g.lda2 + 8 * shalf - g.ksplit;
   const __bf16* pw = Wpl + (long)(n0 + srow) * g.K + 8 * shalf;
-  // fp16x2 with row-scaled A: 2^-e for the staged row, 2^e for the lane's output rows
-  float sscale = 1.0f;
-  if (AR == 1 && g.arowmax) {
-    int e = 0;
-    const float m = __uint_as_float(g.arowmax[ar]);
-    if (m > 0.f) frexpf(m, &e);
-    sscale = ldexpf(1.0f, -e);
-  }
   // two register sets: the global loads of K-tile t+2 are issued while tile t is
   // computed and tile t+1 is converted into LDS (two tiles of latency cover)
   f32x4 ra0[2], ra1[2];
@@ -349,32 +331,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
   auto lstore = [&](int set, int st) {
     __bf16* S = lsm + st * 2 * NP * LPLANE;
     const int off = srow * XLP + 8 * shalf;
-    if (AR == 0) {
-      bf16x8 hh, mm, ll;
+    bf16x8 hh, mm, ll;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        __bf16 a, b, c;
-        split3(ra0[set][e], a, b, c);
-        hh[e] = a; mm[e] = b; ll[e] = c;
-        split3(ra1[set][e], a, b, c);
-        hh[4 + e] = a; mm[4 + e] = b; ll[4 + e] = c;
-      }
-      *reinterpret_cast<bf16x8*>(S + 0 * LPLANE + off) = hh;
-      *reinterpret_cast<bf16x8*>(S + 1 * LPLANE + off) = mm;
-      *reinterpret_cast<bf16x8*>(S + 2 * LPLANE + off) = ll;
-    } else {
-      f16x8 hh, ll;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        _Float16 x0, x1;
-        split2h(ra0[set][e] * sscale, x0, x1);
-        hh[e] = x0; ll[e] = x1;
-        split2h(ra1[set][e] * sscale, x0, x1);
-        hh[4 + e] = x0; ll[4 + e] = x1;
-      }
-      *reinterpret_cast<f16x8*>(S + 0 * LPLANE + off) = hh;
-      *reinterpret_cast<f16x8*>(S + 1 * LPLANE + off) = ll;
+    for (int e = 0; e < 4; ++e) {
+      __bf16 a, b, c;
+      split3(ra0[set][e], a, b, c);
+      hh[e] = a; mm[e] = b; ll[e] = c;
+      split3(ra1[set][e], a, b, c);
+      hh[4 + e] = a; mm[4 + e] = b; ll[4 + e] = c;
     }
+    *reinterpret_cast<bf16x8*>(S + 0 * LPLANE + off) = hh;
+    *reinterpret_cast<bf16x8*>(S + 1 * LPLANE + off) = mm;
+    *reinterpret_cast<bf16x8*>(S + 2 * LPLANE + off) = ll;
 #pragma unroll
     for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(S + (NP + p) * LPLANE + off) = rw[set][p];
   };
@@ -384,50 +352,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
   // accumulators hold C^T tiles (lane = output row, registers = columns)
   auto compute = [&](int st) {
     const __bf16* S = lsm + st * 2 * NP * LPLANE;
-    if (AR == 0) {
-      bf16x8 a[3][2];
+    bf16x8 a[3][2];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          a[p][i] = *reinterpret_cast<const bf16x8*>(S + p * LPLANE + (wm * 64 + i * 32 + r32) * XLP + 8 * h);
-      // W plane 2 pairs with A0; W plane 1 with A1, A0; W plane 0 with A2, A1, A0 (small terms first)
+      for (int i = 0; i < 2; ++i)
+        a[p][i] = *reinterpret_cast<const bf16x8*>(S + p * LPLANE + (wm * 64 + i * 32 + r32) * XLP + 8 * h);
+    // W plane 2 pairs with A0; W plane 1 with A1, A0; W plane 0 with A2, A1, A0 (small terms first)
 #pragma unroll
-      for (int p = 2; p >= 0; --p) {
-        bf16x8 w[4];
+    for (int p = 2; p >= 0; --p) {
+      bf16x8 w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[j] = *reinterpret_cast<const bf16x8*>(S + (3 + p) * LPLANE + (wn * 128 + j * 32 + r32) * XLP + 8 * h);
+      for (int j = 0; j < 4; ++j)
+        w[j] = *reinterpret_cast<const bf16x8*>(S + (3 + p) * LPLANE + (wn * 128 + j * 32 + r32) * XLP + 8 * h);
 #pragma unroll
-        for (int q = 2 - p; q >= 0; --q)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[j], a[q][i], acc[i][j], 0, 0, 0);
-      }
-    } else {
-      f16x8 a[2][2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
+      for (int q = 2 - p; q >= 0; --q)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          a[p][i] = *reinterpret_cast<const f16x8*>(S + p * LPLANE + (wm * 64 + i * 32 + r32) * XLP + 8 * h);
-      // W plane 1 pairs with A0; W plane 0 with A1 then A0 (small terms first)
 #pragma unroll
-      for (int p = 1; p >= 0; --p) {
-        f16x8 w[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w[j] = *reinterpret_cast<const f16x8*>(S + (2 + p) * LPLANE + (wn * 128 + j * 32 + r32) * XLP + 8 * h);
-#pragma unroll
-        for (int q = 1 - p; q >= 0; --q)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[j], a[q][i], acc[i][j], 0, 0, 0);
-      }
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[j], a[q][i], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -455,30 +399,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
 
   // lane l owns output row wm*64 + i*32 + (l & 31) and, per 4-register group q,
   // the four consecutive columns wn*128 + j*32 + 8q + 4h .. +3
-  if (AR == 1) {  // undo the power-of-two scales of the W rows and A rows (exact)
-    float rs[2] = {1.0f, 1.0f};
-    if (g.arowmax) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const long lr = wm * 64 + i * 32 + r32;
-        const long r = row0 + (lr < nrows ? lr : nrows - 1);
-        int e = 0;
-        const float m = __uint_as_float(g.arowmax[r]);
-        if (m > 0.f) frexpf(m, &e);
-        rs[i] = ldexpf(1.0f, e);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] *= sc[e] * rs[i];
-      }
-  }
   if (EPI == EPI_SEGMEAN) {
     // two passes of 128 columns: the wn-th half of the waves writes SiLU(acc + b2) to an
     // LDS tile [256][132], then every thread sums node segments of one column in edge order
@@ -526,7 +446,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
       const long ii = g.ei[row], jj = g.ej[row];
       for (int c = 0; c < g.npairs; ++c) {
         const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-        float mx = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -536,15 +455,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
             const f32x4 qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
             f32x4 v;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v[e] = silu_fast((acc[i][j][4 * q + e] + p[e]) + qv[e]);
-              mx = fmaxf(mx, fabsf(v[e]));
-            }
+            for (int e = 0; e < 4; ++e) v[e] = silu_fast((acc[i][j][4 * q + e] + p[e]) + qv[e]);
             *reinterpret_cast<f32x4*>(g.C + ((long)c * g.E + row) * g.ldc + col) = v;
           }
-        // row maximum of |S| for the next GEMM's fp16 row scaling (lanes h = 0, 1 share the row)
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        if (g.crowmax && h == 0) atomicMax(g.crowmax + (long)c * g.E + row, __float_as_uint(mx));
       }
     } else {
 #pragma unroll
@@ -566,35 +479,23 @@ __global__ __launch_bounds__(512, 1) void k_gemm3_big(GemmArgs g) {
   }
 }
 
-constexpr size_t kBigLds = 2 * 6 * LPLANE * sizeof(__bf16);   // 147456 B (bf16x3)
-constexpr size_t kBigLdsH = 2 * 4 * LPLANE * sizeof(__bf16);  //  98304 B (fp16x2)
-constexpr size_t kSegLds = (size_t)LBM * 132 * sizeof(float);   // 135168 B: EPI_SEGMEAN's [256][132] tile
-static_assert(kSegLds <= kBigLds, "the bf16x3 staging area holds the segment tile");
-constexpr size_t big_lds(int epi, int ar) {
-  return ar == 0 ? kBigLds : (epi == EPI_SEGMEAN ? kSegLds : kBigLdsH);
-}
+constexpr size_t kBigLds = 2 * 6 * LPLANE * sizeof(__bf16);  // 147456 B (also holds EPI_SEGMEAN's [256][132] tile)
+static_assert((size_t)LBM * 132 * sizeof(float) <= kBigLds, "segment tile fits the staging area");
 
 // opt the large dynamic-LDS kernels in; called at model creation, outside any
 // stream capture (a function attribute call is not a stream operation)
 hipError_t gemm_init() {
-  const void* k3[] = {(const void*)k_gemm3_big<EPI_STD, 0>, (const void*)k_gemm3_big<EPI_EDGE, 0>,
-                      (const void*)k_gemm3_big<EPI_SEGMEAN, 0>};
-  const void* k2[] = {(const void*)k_gemm3_big<EPI_STD, 1>, (const void*)k_gemm3_big<EPI_EDGE, 1>,
-                      (const void*)k_gemm3_big<EPI_SEGMEAN, 1>};
-  const int epis[] = {EPI_STD, EPI_EDGE, EPI_SEGMEAN};
-  for (int i = 0; i < 3; ++i) {
-    hipError_t e = hipFuncSetAttribute(k3[i], hipFuncAttributeMaxDynamicSharedMemorySize, big_lds(epis[i], 0));
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(k2[i], hipFuncAttributeMaxDynamicSharedMemorySize, big_lds(epis[i], 1));
+  const void* ks[] = {(const void*)k_gemm3_big<EPI_STD>, (const void*)k_gemm3_big<EPI_EDGE>,
+                      (const void*)k_gemm3_big<EPI_SEGMEAN>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBigLds);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
-template <int AR>
-static hipError_t launch_big(const GemmArgs& g, int epi, hipStream_t s) {
+hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) {
   if (g.N % LBN || g.K % XBK || !g.Wp3 || g.ksplit % XBK || g.gb) return hipErrorInvalidValue;
-  if (AR == 1 && !g.wscale) return hipErrorInvalidValue;
   long blocks;
   if (epi == EPI_SEGMEAN) {
     if (g.N != H || !g.tiles || !g.agg) return hipErrorInvalidValue;
@@ -609,49 +510,15 @@ static hipError_t launch_big(const GemmArgs& g, int epi, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const size_t lds = big_lds(epi, AR);
   if (epi == EPI_EDGE)
-    hipLaunchKernelGGL((k_gemm3_big<EPI_EDGE, AR>), dim3((unsigned)blocks), dim3(512), lds, s, g);
+    hipLaunchKernelGGL((k_gemm3_big<EPI_EDGE>), dim3((unsigned)blocks), dim3(512), kBigLds, s, g);
   else if (epi == EPI_SEGMEAN)
-    hipLaunchKernelGGL((k_gemm3_big<EPI_SEGMEAN, AR>), dim3((unsigned)blocks), dim3(512), lds, s, g);
+    hipLaunchKernelGGL((k_gemm3_big<EPI_SEGMEAN>), dim3((unsigned)blocks), dim3(512), kBigLds, s, g);
   else
-    hipLaunchKernelGGL((k_gemm3_big<EPI_STD, AR>), dim3((unsigned)blocks), dim3(512), lds, s, g);
+    hipLaunchKernelGGL((k_gemm3_big<EPI_STD>), dim3((unsigned)blocks), dim3(512), kBigLds, s, g);
   return hipGetLastError();
 }
 
-hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) { return launch_big<0>(g, epi, s); }
-hipError_t gemm_fp16x2_big(const GemmArgs& g, int epi, hipStream_t s) { return launch_big<1>(g, epi, s); }
-
-// W [N][K] -> two fp16 planes [2][N][K] of W * 2^-e_n with e_n = the exponent of max_k |W[n][k]|
-// (so every scaled entry is <= 1 in magnitude) and wscale[n] = 2^e_n. One block per row.
-__global__ __launch_bounds__(256) void k_split_planes_h(const float* __restrict__ W, int N, int K,
-                                                         _Float16* __restrict__ out, float* __restrict__ wscale) {
-  __shared__ float red[4];
-  const int n = blockIdx.x;
-  const float* row = W + (long)n * K;
-  float m = 0.f;
-  for (int k = threadIdx.x; k < K; k += 256) m = fmaxf(m, fabsf(row[k]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  int e = 0;
-  if (m > 0.f) frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
-  const float sc = ldexpf(1.0f, -e), inv = ldexpf(1.0f, e);
-  for (int k = threadIdx.x; k < K; k += 256) {
-    _Float16 h, l;
-    split2h(row[k] * sc, h, l);
-    out[(long)n * K + k] = h;
-    out[(long)N * K + (long)n * K + k] = l;
-  }
-  if (threadIdx.x == 0) wscale[n] = inv;
-}
-
-hipError_t split_planes_h(const float* W, int N, int K, void* out, float* wscale, hipStream_t s) {
-  hipLaunchKernelGGL(k_split_planes_h, dim3(N), dim3(256), 0, s, W, N, K, reinterpret_cast<_Float16*>(out), wscale);
-  return hipGetLastError();
-}
 
 template <int PF, int REMAP>
 static void launch3(const GemmArgs& g, int epi, long blocks, hipStream_t s) {
