@@ -113,6 +113,28 @@ def cpu_baseline(n_samples, n_atoms, steps):
             "s_per_step": dt}
 
 
+def _pmc_traffic(math):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>/traffic.json;
+    FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE). The counters cannot be
+    read from inside this process, so the value is the one measured on the same command."""
+    if math != "split16":
+        return None, None
+    here = os.path.dirname(os.path.abspath(__file__))
+    for rnd in sorted(os.listdir(os.path.join(here, "profiles")), reverse=True) if os.path.isdir(
+            os.path.join(here, "profiles")) else []:
+        f = os.path.join(here, "profiles", rnd, "traffic.json")
+        if os.path.isfile(f):
+            try:
+                ks = json.load(open(f))["kernels"]
+                for name, v in ks.items():
+                    if "k_edge_gemm<2" in name:
+                        return v["bytes_per_launch"], f"profiles/{rnd}/traffic.json ({name})"
+            except Exception:  # noqa: BLE001
+                return None, None
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,6 +225,9 @@ def main():
     seg_bytes = 2.0 * (E * H * 4 + N * H * 4)
     step_flops = 2 * decoder_pair_flops(natoms)
     math = model.decoder.get_math()
+    fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
+    fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
+    traffic, traffic_src = _pmc_traffic(math)
     # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
     # = bf16 rate) / 3 products; f32 = the fp32 MFMA peak
     peak = {"bf16x3": BF16X3_PEAK_TFLOPS, "split16": MFMA_BF16_PEAK_TFLOPS / 3}.get(math, MFMA_F32_PEAK_TFLOPS)
@@ -252,10 +277,14 @@ def main():
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
-                     "kernel": ("edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), both conditionings"
-                                if math != "f32" else "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"),
+                     "kernel": {"split16": "edge message GEMM + fused scatter_mean (k_edge_gemm<EPI_SEGMEAN>), "
+                                           "both conditionings",
+                                "bf16x3": "edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), "
+                                          "both conditionings",
+                                "f32": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"}[math],
                      "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
-                     "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": None,
+                     "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
                                    "split16": "fp32-equivalent flops; fp16 dense MFMA 2.5 PF / 3 products",
                                    "f32": "fp32 MFMA dense peak"}[math],
@@ -268,6 +297,10 @@ def main():
                     "note": ("in the sampler the aggregation is fused into the message GEMM epilogue; this is the "
                              "standalone kernel on the same [2,E,512] shape" if math != "f32" else
                              "the kernel as launched by the sampler")},
+        "edge_layer1": {"kernel": "edge layer 1 (D.f + P_i + Q_j + SiLU, S written split), both conditionings",
+                        "achieved": fou_tflops, "peak": peak, "unit": "TFLOP/s",
+                        "frac": (fou_tflops / peak) if fou_tflops else None, "flops_per_launch": fou_flops,
+                        "avg_ms": ms_fou / nfou if nfou else None},
         "path": {"tflops": step_flops / s_per_step / 1e12, "mfma_frac": step_flops / s_per_step / 1e12 / peak,
                  "math": math, "flops_per_step_per_gpu": step_flops,
                  "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,

@@ -62,6 +62,7 @@ struct EdgeArgs {
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
+hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // microbenchmarks
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
 

@@ -66,7 +66,9 @@ __device__ __forceinline__ int exp_of(float m) {
 
 }  // namespace
 
-template <int EPI, bool ASC>
+// VAR (microbenchmark variants of the main-loop schedule; the product uses 0):
+//   1 = no s_setprio around the MFMA groups, 2 = A loads issued between the MFMA groups
+template <int EPI, bool ASC, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -103,7 +105,9 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   const char* Ablk = Ab + row0 * rowB;
   const char* Wblk = Wb + (long)n0 * rowB;
   const int lr0 = wave * 32 + (lane >> 3);
-  const unsigned lc16 = 16u * (unsigned)((lane & 7) ^ ((lr0 >> 1) & 7));  // (r >> 1) & 7 is the same for r + 8q
+  // swz(r + 8q) = ((r >> 1) + 4q) & 7 = swz(r) ^ 4 (q & 1): the chunk offset alternates with q
+  const unsigned lc16 = 16u * (unsigned)((lane & 7) ^ ((lr0 >> 1) & 7));
+  const unsigned lc16x = lc16 ^ 64u;
   // (the per-row A offsets are recomputed at each issue: hoisted, they cost 4 VGPRs the
   // main loop does not have)
   int lr0v = lr0;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = lr0v + q * 8;
-      const unsigned off = (unsigned)((r < nrows ? r : (int)nrows - 1) * (int)rowB) + lcv;
+      const unsigned off = (unsigned)((r < nrows ? r : (int)nrows - 1) * (int)rowB) + ((q & 1) ? (lcv ^ 64u) : lcv);
       __builtin_amdgcn_global_load_lds((gbl_void*)(src + off), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
     }
   };
@@ -128,7 +132,8 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     char* d = dst + W_RING + (t % NSW) * OPND_B;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq)), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq + ((q & 1) ? (lc16x - lc16) : 0u))),
+                                       (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
   };
 
   // ---- row exponents of the A chunks (edge layer 2)
@@ -167,25 +172,20 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
       for (int j = 0; j < 4; ++j) fw_[set][p][j] = *reinterpret_cast<const f16x8*>(SW + fw + j * 32 * ROW_B + ch);
     }
   };
+  auto mfma_group = [&](int set, int pw, int pa) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][pw][j], fa_[set][pa][i], acc[i][j], 0, 0, 0);
+  };
   auto mfmas = [&](int set) {
-    __builtin_amdgcn_s_setprio(1);
+    if (VAR != 1) __builtin_amdgcn_s_setprio(1);
     // small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][1][j], fa_[set][0][i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][0][j], fa_[set][1][i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fw_[set][0][j], fa_[set][0][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mfma_group(set, 1, 0);
+    mfma_group(set, 0, 1);
+    mfma_group(set, 0, 0);
+    if (VAR != 1) __builtin_amdgcn_s_setprio(0);
   };
   auto rescale = [&](int t) {
     if (ASC && t > 0 && (t * BK) % CHUNK == 0) {
@@ -224,6 +224,19 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this thread's part of tile t+1 has landed
     if (!(g.dbg & 2)) __builtin_amdgcn_s_barrier();   // everyone's has; tile t's stages are free
     asm volatile("" ::: "memory");
+    if (VAR == 2) {
+      if (!(g.dbg & 1)) issueW(t + 2);
+      read_frags(0, t + 1, 0);
+      __builtin_amdgcn_s_setprio(1);
+      mfma_group(1, 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(g.dbg & 1)) issueA(t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_group(1, 0, 1);
+      mfma_group(1, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      continue;
+    }
     if (!(g.dbg & 1)) {
       issueW(t + 2);
       issueA(t + 3);
@@ -389,6 +402,26 @@ hipError_t edge_gemm_init() {
   return hipSuccess;
 }
 
+hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s) {
+  const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false, 1>, (const void*)k_edge_gemm<EPI_STD, false, 2>};
+  static bool attr = false;
+  if (!attr) {
+    for (const void* k : ks) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
+      if (e != hipSuccess) return e;
+    }
+    attr = true;
+  }
+  const long blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
+  if (var == 1)
+    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 1>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
+  else if (var == 2)
+    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 2>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
+  else
+    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 0>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
+  return hipGetLastError();
+}
+
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
   if (g.N % BN || g.K % BK || !g.A || !g.W || !g.wscale) return hipErrorInvalidValue;
   const bool asc = g.aexp != nullptr;
@@ -418,28 +451,6 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
   else
     hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false>), grid, block, LDS_B, s, g);
   return hipGetLastError();
-}
-
-// Fourier features (cspnet.py:38-52 as k_fourier) written split, rows [768/32][hi 32 | lo 32].
-__global__ void k_fourier_h(const float* __restrict__ x, const int* __restrict__ ei, const int* __restrict__ ej,
-                            long E, _Float16* __restrict__ F) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= E * 3 * NF) return;
-  const long e = idx / (3 * NF);
-  const int r = (int)(idx - e * 3 * NF);
-  const int a = r / NF, k = r - a * NF;
-  // torch.remainder(d, 1.0): fmod, negatives shifted by +1 (k_fourier's rem1)
-  float d = fmodf(__fsub_rn(x[(long)ej[e] * 3 + a], x[(long)ei[e] * 3 + a]), 1.0f);
-  if (d < 0.0f) d = __fadd_rn(d, 1.0f);
-  const float arg = __fmul_rn(d, __fmul_rn(6.28318548202514648f, (float)k));
-  const float sv = sinf(arg), cv = cosf(arg);
-  _Float16* f = F + e * (2 * FD);  // row layout [FD/32][hi 32 | lo 32]
-  const _Float16 sh = (_Float16)sv, ch = (_Float16)cv;
-  const int rs = (r / 32) * 64 + r % 32, rc = ((3 * NF + r) / 32) * 64 + r % 32;
-  f[rs] = sh;
-  f[rs + 32] = (_Float16)(sv - (float)sh);
-  f[rc] = ch;
-  f[rc + 32] = (_Float16)(cv - (float)ch);
 }
 
 // W [N][K] -> split rows [N][K/32][hi 32 | lo 32] of W * 2^-e_n, e_n the exponent of
@@ -477,8 +488,40 @@ hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, 
   return hipGetLastError();
 }
 
+// Fourier features (cspnet.py:38-52 as k_fourier) written split, rows [768/32][hi 32 | lo 32].
+// One thread per (edge, axis, 8 consecutive frequencies): 8 sincosf, four 16-B stores.
+__global__ __launch_bounds__(256) void k_fourier_h(const float* __restrict__ x, const int* __restrict__ ei,
+                                                   const int* __restrict__ ej, long E, _Float16* __restrict__ F) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int G = NF / 8;  // groups of 8 frequencies per axis
+  if (idx >= E * 3 * G) return;
+  const long e = idx / (3 * G);
+  const int r = (int)(idx - e * 3 * G);
+  const int a = r / G, k0 = (r - a * G) * 8;
+  // torch.remainder(d, 1.0): fmod, negatives shifted by +1 (k_fourier's rem1)
+  float d = fmodf(__fsub_rn(x[(long)ej[e] * 3 + a], x[(long)ei[e] * 3 + a]), 1.0f);
+  if (d < 0.0f) d = __fadd_rn(d, 1.0f);
+  f16x8 sh, sl, ch, cl;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const float arg = __fmul_rn(d, __fmul_rn(6.28318548202514648f, (float)(k0 + u)));
+    float sv, cv;
+    sincosf(arg, &sv, &cv);
+    sh[u] = (_Float16)sv;
+    sl[u] = (_Float16)(sv - (float)sh[u]);
+    ch[u] = (_Float16)cv;
+    cl[u] = (_Float16)(cv - (float)ch[u]);
+  }
+  _Float16* f = F + e * (2 * FD);
+  const int cs = a * NF + k0, cc = 3 * NF + a * NF + k0;  // feature columns (8-aligned, inside one 32-chunk)
+  *reinterpret_cast<f16x8*>(f + (cs / 32) * 64 + cs % 32) = sh;
+  *reinterpret_cast<f16x8*>(f + (cs / 32) * 64 + 32 + cs % 32) = sl;
+  *reinterpret_cast<f16x8*>(f + (cc / 32) * 64 + cc % 32) = ch;
+  *reinterpret_cast<f16x8*>(f + (cc / 32) * 64 + 32 + cc % 32) = cl;
+}
+
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s) {
-  const long n = E * 3 * NF;
+  const long n = E * 3 * (NF / 8);
   hipLaunchKernelGGL(k_fourier_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ei, ej, E,
                      reinterpret_cast<_Float16*>(F));
   return hipGetLastError();

@@ -82,6 +82,12 @@ int main(int argc, char** argv) {
     float t0 = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
     printf("M=%ld K=%d glds edge GEMM: %.3f ms %.1f TF fp32-eq; without C stores %.3f ms %.1f TF\n", M, K, te,
            flops / te / 1e9, t0, flops / t0 / 1e9);
+    ea.C = nullptr;
+    for (int rep = 0; rep < 3; ++rep)
+      for (int var = 0; var < 3; ++var) {
+        float tv = time_it(5, s, [&] { CK(edge_gemm_variant(ea, var, s)); });
+        printf("  variant %d (no C): %.3f ms %.1f TF\n", var, tv, flops / tv / 1e9);
+      }
     for (int dbg = 1; dbg < 4; ++dbg) {
       ea.dbg = dbg;
       float td = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
