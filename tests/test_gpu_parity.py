@@ -72,6 +72,18 @@ def cn():
 
 
 # --------------------------------------------------------------------------- kernels
+@pytest.fixture(autouse=True)
+def _default_math(request):
+    """Every test starts and ends in the default arithmetic (split16); tests that compare
+    modes set them explicitly."""
+    models = [request.getfixturevalue(n) for n in ("model100", "model1000") if n in request.fixturenames]
+    for m in models:
+        m.decoder.set_math("split16")
+    yield
+    for m in models:
+        m.decoder.set_math("split16")
+
+
 def test_fourier_features(model1000, golden):
     g = golden("decoder_ragged.npz")
     nat = g["natoms"].tolist()

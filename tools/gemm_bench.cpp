@@ -55,7 +55,7 @@ static float time_it(int reps, hipStream_t s, const std::function<void()>& f) {
 
 int main(int argc, char** argv) {
   const long M = argc > 1 ? atol(argv[1]) : 2L * 819200;  // rows (2E for the message GEMM)
-  const int N = 512;
+  const int N = argc > 4 ? atoi(argv[4]) : 512;
   const int K = argc > 2 ? atoi(argv[2]) : 512;
   hipStream_t s; CK(hipStreamCreate(&s));
   float *A, *W, *C, *bias;
