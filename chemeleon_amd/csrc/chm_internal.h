@@ -49,6 +49,7 @@ struct EdgeArgs {
   float* C; long ldc;            // EPI_STD output
   // EPI_EDGE: S[c][e] = SiLU(acc + PQ[c][ei[e]][:H] + PQ[c][ej[e]][H:]) written as scaled fp16 planes
   const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
+  const int* node_off;           // EPI_EDGE: first node of each graph (with natoms, n2g)
   void* S; int* sexp;            // S as split rows [P*E][H/32][2][32] (columns permuted within each
                                  // 32-chunk, see edge_gemm.hip) + packed chunk exponents
   // EPI_SEGMEAN: agg[c][node] = mean over the node's edges of SiLU(acc + bias)
@@ -57,6 +58,7 @@ struct EdgeArgs {
   const long* node_estart;
   const int* natoms; const int* n2g;
   float* agg;
+  int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers,
             // bit 2 = no epilogue stores (EDGE / SEGMEAN), bit 3 = no PQ loads (EDGE)
 };

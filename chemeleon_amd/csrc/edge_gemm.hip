@@ -26,6 +26,8 @@
 // reads (lanes 0-15 = rows 0-15, one k-half) cover all 64 banks.
 #include "chm_internal.h"
 
+#include <type_traits>
+
 namespace chm {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -47,6 +49,9 @@ constexpr int SEG_TP = 132;                 // EPI_SEGMEAN column tile pitch (fl
 constexpr int SEG_B = BM * SEG_TP * 4;      // 135168 B
 constexpr int LDS_B = RING_B > SEG_B ? RING_B : SEG_B;
 constexpr int CHUNK = 128;                  // S scale granularity (columns)
+constexpr int PQ_PITCH = 260;               // EPI_EDGE staged P / Q rows (floats)
+constexpr int PQ_OFF = 0;
+constexpr int PQ_ROWS = (LDS_B - PQ_OFF) / (PQ_PITCH * 4);
 
 __device__ __forceinline__ float silu_e(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
@@ -93,6 +98,13 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     nrows = g.M - row0 < BM ? g.M - row0 : BM;
   }
   const int K = g.K, nk = K / BK;
+  // Every block of a launch does the same work, so CUs that start together stay in lockstep and
+  // their epilogues (S / agg stores, VALU-only) coincide: the store bursts then saturate HBM while
+  // no CU computes. Holding back every other CU of the first round by about half a tile
+  // (blocks 0-255 take one CU each; XCD = block % 8) keeps half the chip in its main loop
+  // whenever the other half is in its epilogue, for the rest of the launch.
+  if (g.stagger > 0 && blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
+    for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
 
   // ---- glds sources. Operand rows are stored [K/32][hi 32 | lo 32] (fp16): the K-tile of a row
   // is one 128-B line. Wave w stages rows 32w..32w+31 of both operands, 8 rows per instruction;
@@ -306,43 +318,93 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     return;
   }
 
-  if (EPI == EPI_STD && !g.C) return;  // (microbenchmark: main loop only)
+  if (EPI == EPI_EDGE) {
+    // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
+    // 128-column chunk (this wave's columns), e from the chunk's max |S|. The tile's rows are
+    // consecutive edges, so they touch few distinct nodes: the P rows of sources [ilo, ihi] and
+    // the Q rows of the targets [jlo, jhi] (whole crystals) are staged into the free ring LDS
+    // (this block's 256 columns, pitch 260 floats: the Q reads of 16 consecutive edges cover all
+    // banks, the P reads broadcast) and read from there; tiles spanning too many nodes (crystals
+    // of <= 3 atoms, crystal-boundary tiles at n > 75) gather from global memory instead.
+    const long rl = row0 + nrows - 1;
+    const int ilo = g.ei[row0], ihi = g.ei[rl];
+    const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
+    const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
+    const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1;
+    const bool staged = nP + nQ <= PQ_ROWS;
+    const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
+    long rowv[2];
+    int pr[2], qr[2];  // staged: LDS rows; gathered: node indices
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long lr = wm * 64 + i * 32 + r32;
-    if (lr >= nrows) continue;
-    const long row = row0 + lr;
-    if (EPI == EPI_EDGE) {
-      // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
-      // 128-column chunk (this wave's columns), e from the chunk's max |S|
-      // S values go through a wave-private LDS tile [32 rows][132] (pitch 132: the 16 lanes of
-      // a ds_write_b128 cover all banks) so the chunk max is known before the split
-      const long ii = g.ei[row], jj = g.ej[row];
-      _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
-      float* V = reinterpret_cast<float*>(lds) + wave * (32 * SEG_TP) + r32 * SEG_TP;
-      for (int c = 0; c < g.npairs; ++c) {
-        const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-        float mx = 0.f;
+    for (int i = 0; i < 2; ++i) {
+      const long lr = wm * 64 + i * 32 + r32;
+      rowv[i] = row0 + (lr < nrows ? lr : nrows - 1);
+      pr[i] = g.ei[rowv[i]];
+      qr[i] = g.ej[rowv[i]];
+      if (staged) {
+        pr[i] -= ilo;
+        qr[i] = nP + qr[i] - jlo;
+      }
+    }
+    _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
+    auto stage = [&](int c) {
+      if (!staged) return;
+      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+      if (c > 0) __syncthreads();  // everyone is done reading conditioning c - 1
+      for (int r = wave; r < nP + nQ; r += 8) {
+        const float* src = Pc + (r < nP ? (long)(ilo + r) * (2 * H) : (long)(jlo + r - nP) * (2 * H) + H) + n0 + 4 * lane;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + PQ_OFF + r * PQ_PITCH * 4), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    // conditioning c; LAST: the final one, whose SiLU values may overwrite acc
+    auto run = [&](int c, auto LAST) {
+      constexpr bool last = decltype(LAST)::value;
+      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const long lr = wm * 64 + i * 32 + r32;  // rows past nrows compute clamped copies, never stored
+        const long row = rowv[i];
+        auto pq = [&](int j, int q, f32x4& p, f32x4& qv) {
+          const int lc = wn * 128 + j * 32 + 8 * q + 4 * h;  // column within the block
+          if (g.dbg & 8) {
+            p = f32x4{0.f, 0.f, 0.f, 0.f};
+            qv = p;
+          } else if (staged) {
+            p = *reinterpret_cast<const f32x4*>(T + pr[i] * PQ_PITCH + lc);
+            qv = *reinterpret_cast<const f32x4*>(T + qr[i] * PQ_PITCH + lc);
+          } else {
+            p = *reinterpret_cast<const f32x4*>(Pc + (long)pr[i] * (2 * H) + n0 + lc);
+            qv = *reinterpret_cast<const f32x4*>(Pc + (long)qr[i] * (2 * H) + H + n0 + lc);
+          }
+        };
+        // SiLU values: conditioning 0 in v (acc is needed again), the last one in place
+        f32x4 v[4][4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int lc = j * 32 + 8 * q + 4 * h;
-            const int col = n0 + wn * 128 + lc;
-            f32x4 p = {0.f, 0.f, 0.f, 0.f}, qv = p;
-            if (!(g.dbg & 8)) {
-              p = *reinterpret_cast<const f32x4*>(Pc + ii * (2 * H) + col);
-              qv = *reinterpret_cast<const f32x4*>(Pc + jj * (2 * H) + H + col);
-            }
-            f32x4 v;
+            f32x4 p, qv;
+            pq(j, q, p, qv);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              v[e] = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
-              mx = fmaxf(mx, fabsf(v[e]));
+              const float x = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
+              if constexpr (last) acc[i][j][4 * q + e] = x;
+              else v[j][q][e] = x;
             }
-            *reinterpret_cast<f32x4*>(V + lc) = v;
-            __builtin_amdgcn_sched_barrier(0);  // bound the PQ loads in flight (register pressure)
           }
+        auto val = [&](int j, int q, int e) {
+          if constexpr (last) return acc[i][j][4 * q + e];
+          else return v[j][q][e];
+        };
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(val(j, q, e)));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // lanes h = 0, 1 share the row
         const int ex2 = exp_of(mx);
         const float sc = ldexpf(1.0f, -ex2);
@@ -350,23 +412,23 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
         _Float16* srow = S0 + orow * (2 * H);  // [H/32][hi 32 | lo 32]
         // S is stored with the columns of each 32-chunk permuted, 8q + 4h + e -> 16h + 4q + e
         // (W2's K index carries the same permutation, split_rows_h(perm)), so a lane's 16 values
-        // of a chunk are contiguous: two 16-B stores per plane
+        // of a chunk are contiguous: two 16-B stores per plane. (Routing the lines through LDS so
+        // that each instruction writes 8 whole lines measured no faster: the store path, ~6 TB/s
+        // chip-wide, not the line count, sets the cost.)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f16x8 hv[2], lv[2];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(V + j * 32 + 8 * q + 4 * h);
+          for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float x = v[e] * sc;
+              const float x = val(j, q, e) * sc;
               const _Float16 hx = (_Float16)x;
               hv[q >> 1][4 * (q & 1) + e] = hx;
               lv[q >> 1][4 * (q & 1) + e] = (_Float16)(x - (float)hx);
             }
-          }
           _Float16* d = srow + ((n0 + wn * 128) / 32 + j) * 64 + 16 * h;
-          if (g.dbg & 4) {  // profiling: keep the values live, store nothing
+          if ((g.dbg & 4) || lr >= nrows) {  // (profiling: keep the values live, store nothing)
             asm volatile("" ::"v"(hv[0]), "v"(hv[1]), "v"(lv[0]), "v"(lv[1]));
             continue;
           }
@@ -375,20 +437,39 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
           *reinterpret_cast<f16x8*>(d + 32) = lv[0];
           *reinterpret_cast<f16x8*>(d + 40) = lv[1];
         }
-        if (h == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+        if (h == 0 && lr < nrows)
+          reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
       }
+    };
+    using F = std::integral_constant<bool, false>;
+    using Tr = std::integral_constant<bool, true>;
+    stage(0);
+    if (g.npairs > 1) {
+      run(0, F{});
+      stage(1);
+      run(1, Tr{});
     } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int col = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
-          f32x4 v;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-          *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
-        }
+      run(0, Tr{});
     }
+    return;
+  }
+
+  if (EPI == EPI_STD && !g.C) return;  // (microbenchmark: main loop only)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 64 + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+      }
   }
 }
 
@@ -432,7 +513,7 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
     blocks = (long)g.ntiles * g.npairs * (g.N / BN);
   } else {
     if (g.M <= 0) return hipErrorInvalidValue;
-    if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || asc)) return hipErrorInvalidValue;
+    if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g || asc)) return hipErrorInvalidValue;
     blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
   }
   static bool attr = false;

@@ -52,6 +52,7 @@ struct chm_model {
   void* mem2 = nullptr;  // fp16 planes + scales arena
   int math = MATH_SPLIT16;
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
+  int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   std::vector<LayerW> layers;
 };
 
@@ -208,6 +209,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->math = mode == "f32" ? MATH_F32 : mode == "bf16x3" ? MATH_BF16X3 : MATH_SPLIT16;
     const char* dbg = getenv("CHM_EDGE_DBG");
     m->edge_dbg = dbg ? atoi(dbg) : 0;
+    const char* stg = getenv("CHM_EDGE_STAGGER");
+    if (stg) m->edge_stagger = atoi(stg);
     struct Job { const float* src; size_t n; const void** dst; };
     std::vector<Job> jobs;
     jobs.push_back({m->Wc, (size_t)2 * H * CIN, &m->Wc3});
@@ -529,7 +532,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         std::memset(&ea, 0, sizeof(ea));
         ea.M = E; ea.N = H; ea.K = FD; ea.A = b->F; ea.W = w.D2h; ea.wscale = w.Dsc;
         ea.ei = b->ei; ea.ej = b->ej; ea.PQ = b->PQ; ea.nnodes = N; ea.npairs = P; ea.E = E;
-        ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg;
+        ea.node_off = b->node_off; ea.natoms = b->natoms; ea.n2g = b->n2g;
+        ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
         HIPCHK(edge_gemm(ea, EPI_EDGE, s));
       }
@@ -539,7 +543,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
         ea.W = w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles; ea.ntiles = b->ntiles;
         ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
-        ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg;
+        ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
         HIPCHK(edge_gemm(ea, EPI_SEGMEAN, s));
       }
