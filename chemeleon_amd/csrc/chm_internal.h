@@ -58,12 +58,15 @@ struct EdgeArgs {
   const long* node_estart;
   const int* natoms; const int* n2g;
   float* agg;
+  unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers,
             // bit 2 = no epilogue stores (EDGE / SEGMEAN), bit 3 = no PQ loads (EDGE)
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
+// two-workgroups-per-CU variant (128x256 tiles), EPI_STD / EPI_EDGE, unscaled A
+hipError_t edge_gemm_pp(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // microbenchmarks
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);

@@ -47,11 +47,10 @@ constexpr int W_RING = NSA * OPND_B;        // W stages follow the A stages
 constexpr int RING_B = (NSA + NSW) * OPND_B;  // 160 KB
 constexpr int SEG_TP = 132;                 // EPI_SEGMEAN column tile pitch (floats)
 constexpr int SEG_B = BM * SEG_TP * 4;      // 135168 B
-constexpr int LDS_B = RING_B > SEG_B ? RING_B : SEG_B;
+constexpr int LDS_B = RING_B > SEG_B + 2048 ? RING_B : SEG_B + 2048;  // (+ the SEGMEAN node list)
 constexpr int CHUNK = 128;                  // S scale granularity (columns)
 constexpr int PQ_PITCH = 260;               // EPI_EDGE staged P / Q rows (floats)
 constexpr int PQ_OFF = 0;
-constexpr int PQ_ROWS = (LDS_B - PQ_OFF) / (PQ_PITCH * 4);
 
 __device__ __forceinline__ float silu_e(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
@@ -62,6 +61,18 @@ __device__ __forceinline__ long remap(long b, long nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+__device__ __forceinline__ unsigned long long rtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+__device__ __forceinline__ unsigned hwid() {
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  return ((xcc & 0xf) << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xf);
+}
+
 // exponent e with m = f 2^e, f in [0.5, 1) (0 for m == 0)
 __device__ __forceinline__ int exp_of(float m) {
   int e = 0;
@@ -70,6 +81,162 @@ __device__ __forceinline__ int exp_of(float m) {
 }
 
 }  // namespace
+
+// Edge layer 1 epilogue, shared by both edge-GEMM kernels: acc holds D f for rows
+// row0 + wm*64 + i*32 + r32 (i = 0, 1), columns n0 + wn*128 + j*32 + 8q + 4h + e, already
+// multiplied by wscale. NW waves, ldsb bytes of free LDS.
+template <int NW>
+__device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2][4], char* lds, int ldsb, int wave,
+                                              int lane, long row0, long nrows, int n0) {
+  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, r32 = lane & 31;
+  const int PQ_ROWS = ldsb / (PQ_PITCH * 4);
+    // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
+    // 128-column chunk (this wave's columns), e from the chunk's max |S|. The tile's rows are
+    // consecutive edges, so they touch few distinct nodes: the P rows of sources [ilo, ihi] and
+    // the Q rows of the targets [jlo, jhi] (whole crystals) are staged into the free ring LDS
+    // (this block's 256 columns, pitch 260 floats: the Q reads of 16 consecutive edges cover all
+    // banks, the P reads broadcast) and read from there; tiles spanning too many nodes (crystals
+    // of <= 3 atoms, crystal-boundary tiles at n > 75) gather from global memory instead.
+    const long rl = row0 + nrows - 1;
+    const int ilo = g.ei[row0], ihi = g.ei[rl];
+    const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
+    const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
+    const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1;
+    const bool staged = nP + nQ <= PQ_ROWS;
+    const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
+    long rowv[2];
+    int pr[2], qr[2];  // staged: LDS rows; gathered: node indices
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long lr = wm * 64 + i * 32 + r32;
+      rowv[i] = row0 + (lr < nrows ? lr : nrows - 1);
+      pr[i] = g.ei[rowv[i]];
+      qr[i] = g.ej[rowv[i]];
+      if (staged) {
+        pr[i] -= ilo;
+        qr[i] = nP + qr[i] - jlo;
+      }
+    }
+    _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
+    // Stores count in vmcnt (gfx9), so a load issued after conditioning 0's S stores and then
+    // waited on would wait for those stores to drain: when both conditionings' rows fit, they are
+    // staged together before any store (rows [c * nR, (c + 1) * nR)).
+    const int nR = nP + nQ;
+    const bool both = staged && g.npairs * nR <= PQ_ROWS;
+    auto stage = [&](int c0, int c1) {  // conditionings [c0, c1)
+      if (!staged) return;
+      if (c0 > 0) __syncthreads();  // everyone is done reading the previous conditioning
+      for (int c = c0; c < c1; ++c) {
+        const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+        const int rb = both ? c * nR : 0;
+        for (int r = wave; r < nR; r += NW) {
+          const float* src = Pc + (r < nP ? (long)(ilo + r) * (2 * H) : (long)(jlo + r - nP) * (2 * H) + H) + n0 + 4 * lane;
+          __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + PQ_OFF + (rb + r) * PQ_PITCH * 4), 16, 0,
+                                           0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    // conditioning c; LAST: the final one, whose SiLU values may overwrite acc; STG: P / Q rows
+    // from the staged LDS image (else gathered from global memory). Both flags are compile-time
+    // so each path is straight-line code.
+    const bool nostore = g.dbg & 4;  // (profiling)
+    auto run = [&](int c, auto LAST, auto STG) {
+      constexpr bool last = decltype(LAST)::value, stg = decltype(STG)::value;
+      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+      const int rb = both ? c * nR : 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const long lr = wm * 64 + i * 32 + r32;  // rows past nrows compute clamped copies, never stored
+        const long row = rowv[i];
+        const float* prow;
+        const float* qrow;
+        if constexpr (stg) {
+          prow = T + (rb + pr[i]) * PQ_PITCH + wn * 128 + 4 * h;
+          qrow = T + (rb + qr[i]) * PQ_PITCH + wn * 128 + 4 * h;
+        } else {
+          prow = Pc + (long)pr[i] * (2 * H) + n0 + wn * 128 + 4 * h;
+          qrow = Pc + (long)qr[i] * (2 * H) + H + n0 + wn * 128 + 4 * h;
+        }
+        // SiLU values: conditioning 0 in v (acc is needed again), the last one in place
+        f32x4 v[4][4];
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 p = *reinterpret_cast<const f32x4*>(prow + j * 32 + 8 * q);
+            const f32x4 qv = *reinterpret_cast<const f32x4*>(qrow + j * 32 + 8 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
+              mx = fmaxf(mx, fabsf(x));
+              if constexpr (last) acc[i][j][4 * q + e] = x;
+              else v[j][q][e] = x;
+            }
+          }
+        auto val = [&](int j, int q, int e) {
+          if constexpr (last) return acc[i][j][4 * q + e];
+          else return v[j][q][e];
+        };
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // lanes h = 0, 1 share the row
+        const int ex2 = exp_of(mx);
+        const float sc = ldexpf(1.0f, -ex2);
+        const long orow = (long)c * g.E + row;
+        _Float16* srow = S0 + orow * (2 * H) + ((n0 + wn * 128) / 32) * 64 + 16 * h;  // [H/32][hi 32 | lo 32]
+        // S is stored with the columns of each 32-chunk permuted, 8q + 4h + e -> 16h + 4q + e
+        // (W2's K index carries the same permutation, split_rows_h(perm)), so a lane's 16 values
+        // of a chunk are contiguous: two 16-B stores per plane. (Routing the lines through LDS so
+        // that each instruction writes 8 whole lines measured no faster.)
+        if (lr < nrows && !nostore) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f16x8 hv[2], lv[2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x = val(j, q, e) * sc;
+                const _Float16 hx = (_Float16)x;
+                hv[q >> 1][4 * (q & 1) + e] = hx;
+                lv[q >> 1][4 * (q & 1) + e] = (_Float16)(x - (float)hx);
+              }
+            _Float16* d = srow + j * 64;
+            *reinterpret_cast<f16x8*>(d) = hv[0];
+            *reinterpret_cast<f16x8*>(d + 8) = hv[1];
+            *reinterpret_cast<f16x8*>(d + 32) = lv[0];
+            *reinterpret_cast<f16x8*>(d + 40) = lv[1];
+          }
+          if (h == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+        }
+      }
+    };
+    using F = std::integral_constant<bool, false>;
+    using Tr = std::integral_constant<bool, true>;
+    auto all = [&](auto STG) {
+      if (g.npairs > 1) {
+        if (both) {
+          stage(0, 2);
+          if (g.trace && threadIdx.x == 0) g.trace[6 * blockIdx.x + 4] = rtime();
+          run(0, F{}, STG);
+          if (g.trace && threadIdx.x == 0) g.trace[6 * blockIdx.x + 5] = rtime();
+        } else {
+          stage(0, 1);
+          run(0, F{}, STG);
+          stage(1, 2);
+        }
+        run(1, Tr{}, STG);
+      } else {
+        stage(0, 1);
+        run(0, Tr{}, STG);
+      }
+    };
+    if (staged)
+      all(Tr{});
+    else
+      all(F{});
+}
 
 // VAR (microbenchmark variants of the main-loop schedule; the product uses 0):
 //   1 = no s_setprio around the MFMA groups, 2 = A loads issued between the MFMA groups
@@ -98,6 +265,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     nrows = g.M - row0 < BM ? g.M - row0 : BM;
   }
   const int K = g.K, nk = K / BK;
+  const unsigned long long t0 = g.trace ? rtime() : 0;
   // Every block of a launch does the same work, so CUs that start together stay in lockstep and
   // their epilogues (S / agg stores, VALU-only) coincide: the store bursts then saturate HBM while
   // no CU computes. Holding back every other CU of the first round by about half a tile
@@ -283,9 +451,32 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   // the four consecutive columns wn*128 + j*32 + 8q + 4h .. +3
   if (EPI == EPI_SEGMEAN) {
     // two passes of 128 columns: the wn-th half of the waves writes SiLU(acc + b2) to an
-    // LDS tile [256][132], then every thread sums node segments of one column in edge order
+    // LDS tile [256][132], then every thread sums node segments of one column in edge order.
+    // The tile's node list (atom count, first row) is fetched while the first pass computes and
+    // kept in LDS after the tile (int2 [<= 256]).
+    if (g.dbg & 128) return;  // (profiling: main loop only)
     float* T = reinterpret_cast<float*>(lds);
+    int2* info = reinterpret_cast<int2*>(lds + SEG_B);
     const long es0 = g.node_estart[seg.x];
+    const int nn = seg.y - seg.x;
+    int2 my = {0, 0};
+    if (tid < nn) {
+      const int nd = seg.x + tid;
+      my.x = g.natoms[g.n2g[nd]];
+      my.y = (int)(g.node_estart[nd] - es0);
+    }
+    // every wave applies bias + SiLU to its accumulators first (all eight waves at once), then the
+    // owners of each 128-column half write it to the tile
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(g.bias + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = silu_e(acc[i][j][4 * q + e] + b[e]);
+      }
     for (int half = 0; half < 2; ++half) {
       if (wn == half) {
 #pragma unroll
@@ -293,25 +484,35 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int col = j * 32 + 8 * q + 4 * h;
-            const f32x4 b = *reinterpret_cast<const f32x4*>(g.bias + n0 + half * 128 + col);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
               const int row = wm * 64 + i * 32 + r32;
               f32x4 v;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = silu_e(acc[i][j][4 * q + e] + b[e]);
+              for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
               *reinterpret_cast<f32x4*>(T + row * SEG_TP + col) = v;
             }
           }
       }
+      if (half == 0 && tid < nn) info[tid] = my;
       __syncthreads();
       const int col = tid & 127;
-      for (int nd = seg.x + (tid >> 7); nd < seg.y; nd += 4) {
-        const int n = g.natoms[g.n2g[nd]];
-        const int r0 = (int)(g.node_estart[nd] - es0);
+      for (int k = tid >> 7; k < nn && !(g.dbg & 256); k += 4) {
+        const int2 ni = info[k];
+        const float* src = T + ni.y * SEG_TP + col;
+        // sequential sum in edge order (scatter_add's order); loads issued eight at a time
         float sacc = 0.f;
-        for (int j = 0; j < n; ++j) sacc += T[(r0 + j) * SEG_TP + col];
-        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + nd) * H + n0 + half * 128 + col] = sacc / (float)(n < 1 ? 1 : n);
+        int j = 0;
+        for (; j + 8 <= ni.x; j += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = src[(j + u) * SEG_TP];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sacc += v[u];
+        }
+        for (; j < ni.x; ++j) sacc += src[j * SEG_TP];
+        if (!(g.dbg & 4))
+          g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = sacc / (float)(ni.x < 1 ? 1 : ni.x);
       }
       __syncthreads();
     }
@@ -319,137 +520,14 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   }
 
   if (EPI == EPI_EDGE) {
-    // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
-    // 128-column chunk (this wave's columns), e from the chunk's max |S|. The tile's rows are
-    // consecutive edges, so they touch few distinct nodes: the P rows of sources [ilo, ihi] and
-    // the Q rows of the targets [jlo, jhi] (whole crystals) are staged into the free ring LDS
-    // (this block's 256 columns, pitch 260 floats: the Q reads of 16 consecutive edges cover all
-    // banks, the P reads broadcast) and read from there; tiles spanning too many nodes (crystals
-    // of <= 3 atoms, crystal-boundary tiles at n > 75) gather from global memory instead.
-    const long rl = row0 + nrows - 1;
-    const int ilo = g.ei[row0], ihi = g.ei[rl];
-    const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
-    const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
-    const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1;
-    const bool staged = nP + nQ <= PQ_ROWS;
-    const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
-    long rowv[2];
-    int pr[2], qr[2];  // staged: LDS rows; gathered: node indices
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const long lr = wm * 64 + i * 32 + r32;
-      rowv[i] = row0 + (lr < nrows ? lr : nrows - 1);
-      pr[i] = g.ei[rowv[i]];
-      qr[i] = g.ej[rowv[i]];
-      if (staged) {
-        pr[i] -= ilo;
-        qr[i] = nP + qr[i] - jlo;
-      }
-    }
-    _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
-    auto stage = [&](int c) {
-      if (!staged) return;
-      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-      if (c > 0) __syncthreads();  // everyone is done reading conditioning c - 1
-      for (int r = wave; r < nP + nQ; r += 8) {
-        const float* src = Pc + (r < nP ? (long)(ilo + r) * (2 * H) : (long)(jlo + r - nP) * (2 * H) + H) + n0 + 4 * lane;
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + PQ_OFF + r * PQ_PITCH * 4), 16, 0, 0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long tm = g.trace ? rtime() : 0;
+    edge_epilogue<8>(g, acc, lds, LDS_B, wave, lane, row0, nrows, n0);
+    if (g.trace) {
       __syncthreads();
-    };
-    // conditioning c; LAST: the final one, whose SiLU values may overwrite acc
-    auto run = [&](int c, auto LAST) {
-      constexpr bool last = decltype(LAST)::value;
-      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const long lr = wm * 64 + i * 32 + r32;  // rows past nrows compute clamped copies, never stored
-        const long row = rowv[i];
-        auto pq = [&](int j, int q, f32x4& p, f32x4& qv) {
-          const int lc = wn * 128 + j * 32 + 8 * q + 4 * h;  // column within the block
-          if (g.dbg & 8) {
-            p = f32x4{0.f, 0.f, 0.f, 0.f};
-            qv = p;
-          } else if (staged) {
-            p = *reinterpret_cast<const f32x4*>(T + pr[i] * PQ_PITCH + lc);
-            qv = *reinterpret_cast<const f32x4*>(T + qr[i] * PQ_PITCH + lc);
-          } else {
-            p = *reinterpret_cast<const f32x4*>(Pc + (long)pr[i] * (2 * H) + n0 + lc);
-            qv = *reinterpret_cast<const f32x4*>(Pc + (long)qr[i] * (2 * H) + H + n0 + lc);
-          }
-        };
-        // SiLU values: conditioning 0 in v (acc is needed again), the last one in place
-        f32x4 v[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            f32x4 p, qv;
-            pq(j, q, p, qv);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
-              if constexpr (last) acc[i][j][4 * q + e] = x;
-              else v[j][q][e] = x;
-            }
-          }
-        auto val = [&](int j, int q, int e) {
-          if constexpr (last) return acc[i][j][4 * q + e];
-          else return v[j][q][e];
-        };
-        float mx = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fabsf(val(j, q, e)));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));  // lanes h = 0, 1 share the row
-        const int ex2 = exp_of(mx);
-        const float sc = ldexpf(1.0f, -ex2);
-        const long orow = (long)c * g.E + row;
-        _Float16* srow = S0 + orow * (2 * H);  // [H/32][hi 32 | lo 32]
-        // S is stored with the columns of each 32-chunk permuted, 8q + 4h + e -> 16h + 4q + e
-        // (W2's K index carries the same permutation, split_rows_h(perm)), so a lane's 16 values
-        // of a chunk are contiguous: two 16-B stores per plane. (Routing the lines through LDS so
-        // that each instruction writes 8 whole lines measured no faster: the store path, ~6 TB/s
-        // chip-wide, not the line count, sets the cost.)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f16x8 hv[2], lv[2];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x = val(j, q, e) * sc;
-              const _Float16 hx = (_Float16)x;
-              hv[q >> 1][4 * (q & 1) + e] = hx;
-              lv[q >> 1][4 * (q & 1) + e] = (_Float16)(x - (float)hx);
-            }
-          _Float16* d = srow + ((n0 + wn * 128) / 32 + j) * 64 + 16 * h;
-          if ((g.dbg & 4) || lr >= nrows) {  // (profiling: keep the values live, store nothing)
-            asm volatile("" ::"v"(hv[0]), "v"(hv[1]), "v"(lv[0]), "v"(lv[1]));
-            continue;
-          }
-          *reinterpret_cast<f16x8*>(d) = hv[0];
-          *reinterpret_cast<f16x8*>(d + 8) = hv[1];
-          *reinterpret_cast<f16x8*>(d + 32) = lv[0];
-          *reinterpret_cast<f16x8*>(d + 40) = lv[1];
-        }
-        if (h == 0 && lr < nrows)
-          reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+      if (tid == 0) {
+        unsigned long long* o = g.trace + 6 * blockIdx.x;
+        o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
       }
-    };
-    using F = std::integral_constant<bool, false>;
-    using Tr = std::integral_constant<bool, true>;
-    stage(0);
-    if (g.npairs > 1) {
-      run(0, F{});
-      stage(1);
-      run(1, Tr{});
-    } else {
-      run(0, Tr{});
     }
     return;
   }
@@ -471,6 +549,204 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
         *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
       }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Two workgroups per CU ("pp"): 256-thread workgroups, 128x256 output tiles, 4 waves of 64x128
+// (the same per-wave accumulators and epilogue as k_edge_gemm), an 80-KB LDS budget each. With
+// one workgroup per CU the epilogue (SiLU / split VALU, S stores at the chip's ~6 TB/s store
+// rate) runs with the matrix cores idle; two resident workgroups that drift out of phase let one
+// workgroup's epilogue run beside the other's MFMAs (the two waves on a SIMD belong to different
+// workgroups). The price: 1.5x the operand bytes per flop (128-row tiles) and one barrier per 24
+// MFMAs.
+// K-tiles of 16: a row's K-tile is 64 B = hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15 (four 16-B
+// pieces taken from the [K/32][hi 32 | lo 32] split rows); piece p of row r sits at p ^ ((r>>2)&3)
+// (conflict-free fragment reads). Ring: 3 stages of A 8 KB + W 16 KB, two K-tiles in flight.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int PP_TM = 128, PP_TN = 256, PP_BK = 16, PP_ROWB = 64;
+constexpr int PP_A = PP_TM * PP_ROWB, PP_W = PP_TN * PP_ROWB, PP_STAGE = PP_A + PP_W, PP_NST = 3;
+constexpr int PP_LDS = 80 * 1024;
+}  // namespace
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void k_edge_pp(EdgeArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int ntn = g.N / PP_TN;
+  const long bid = remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(bid % ntn) * PP_TN;
+  const long row0 = (bid / ntn) * PP_TM;
+  const long nrows = g.M - row0 < PP_TM ? g.M - row0 : PP_TM;
+  const int K = g.K, nk = K / PP_BK;
+  if (g.stagger > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
+  const unsigned long long t0 = g.trace ? rtime() : 0;
+
+  // ---- glds: instruction q of a wave covers 16 rows (lane L: row (L >> 2), LDS piece L & 3,
+  // logical piece (L & 3) ^ ((L >> 4) & 3)); A rows 32w + 16q (q < 2), W rows 64w + 16q (q < 4)
+  const char* Ab = reinterpret_cast<const char*>(g.A);
+  const char* Wb = reinterpret_cast<const char*>(g.W);
+  const long rowB = (long)K * 4;
+  const int lp = (lane & 3) ^ ((lane >> 4) & 3);
+  const unsigned poff = 16u * (lp & 1) + 64u * (lp >> 1);
+  unsigned aoff[2], woff[4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 32 * wave + 16 * q + (lane >> 2);
+    aoff[q] = (unsigned)((r < nrows ? r : (int)nrows - 1) * rowB) + poff;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) woff[q] = (unsigned)((64 * wave + 16 * q + (lane >> 2)) * rowB) + poff;
+  const char* Ablk = Ab + row0 * rowB;
+  const char* Wblk = Wb + (long)n0 * rowB;
+  auto issue = [&](int t) {
+    const int tt = t < nk ? t : nk - 1;  // past the end: re-read the last tile into an idle stage
+    const long kb = (long)(tt >> 1) * 128 + 32 * (tt & 1);
+    char* st = lds + (t % PP_NST) * PP_STAGE;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(Ablk + kb + aoff[q]), (lds_void*)(st + (32 * wave + 16 * q) * PP_ROWB),
+                                       16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(Wblk + kb + woff[q]),
+                                       (lds_void*)(st + PP_A + (64 * wave + 16 * q) * PP_ROWB), 16, 0, 0);
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  const int swz = (r32 >> 2) & 3;
+  const int chh = 16 * (h ^ swz), chl = 16 * ((2 + h) ^ swz);  // hi / lo fragment pieces
+  const int fa = (wm * 64 + r32) * PP_ROWB, fw = (wn * 128 + r32) * PP_ROWB;
+
+  // fragments double-buffered across K-tiles: while the MFMAs of tile t run, the fragments of
+  // tile t+1 are read and the loads of tile t+3 are issued, both interleaved between the MFMAs
+  f16x8 fr[2][12];  // [set][ah0 ah1 al0 al1 | wh0..3 | wl0..3]
+  auto read_frags = [&](int set, int t) {
+    const char* st = lds + (t % PP_NST) * PP_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      fr[set][i] = *reinterpret_cast<const f16x8*>(st + fa + i * 32 * PP_ROWB + chh);
+      fr[set][2 + i] = *reinterpret_cast<const f16x8*>(st + fa + i * 32 * PP_ROWB + chl);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fr[set][4 + j] = *reinterpret_cast<const f16x8*>(st + PP_A + fw + j * 32 * PP_ROWB + chh);
+      fr[set][8 + j] = *reinterpret_cast<const f16x8*>(st + PP_A + fw + j * 32 * PP_ROWB + chl);
+    }
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_frags(0, 0);
+  // tile t uses fragment set t & 1; the loop is unrolled by two so the sets stay in registers
+  auto step = [&](int t, auto CUR) {
+    constexpr int cur = decltype(CUR)::value;
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // this thread's part of tile t+1 has landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): tile t's fragments are in
+    __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage is free
+    asm volatile("" ::: "memory");
+    issue(t + 3);                                     // past the end: re-reads into the free stage
+    read_frags(cur ^ 1, t + 1);                       // past the end: reads a re-read tile
+    __builtin_amdgcn_s_setprio(1);
+    // small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][8 + j], fr[cur][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][4 + j], fr[cur][2 + i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][4 + j], fr[cur][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  for (int t = 0; t < nk; t += 2) {  // nk = K / 16 is even
+    step(t, std::integral_constant<int, 0>{});
+    step(t + 1, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] *= sc[e];
+    }
+  if (EPI == EPI_EDGE) {
+    const unsigned long long tm = g.trace ? rtime() : 0;
+    edge_epilogue<4>(g, acc, lds, PP_LDS, wave, lane, row0, nrows, n0);
+    if (g.trace) {
+      __syncthreads();
+      if (tid == 0) {
+        unsigned long long* o = g.trace + 6 * blockIdx.x;
+        o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
+      }
+    }
+    return;
+  }
+  if (!g.C) return;  // (microbenchmark: main loop only)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 64 + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+      }
+  }
+}
+
+hipError_t edge_gemm_pp(const EdgeArgs& g, int epi, hipStream_t s) {
+  if (g.N % PP_TN || g.K % 32 || !g.A || !g.W || !g.wscale || g.aexp || g.M <= 0) return hipErrorInvalidValue;
+  if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g))
+    return hipErrorInvalidValue;
+  if (epi != EPI_EDGE && epi != EPI_STD) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    const void* ks[] = {(const void*)k_edge_pp<EPI_STD>, (const void*)k_edge_pp<EPI_EDGE>};
+    for (const void* k : ks) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+      if (e != hipSuccess) return e;
+    }
+    attr = true;
+  }
+  const long blocks = ((g.M + PP_TM - 1) / PP_TM) * (g.N / PP_TN);
+  if (epi == EPI_EDGE)
+    hipLaunchKernelGGL(k_edge_pp<EPI_EDGE>, dim3((unsigned)blocks), dim3(256), PP_LDS, s, g);
+  else
+    hipLaunchKernelGGL(k_edge_pp<EPI_STD>, dim3((unsigned)blocks), dim3(256), PP_LDS, s, g);
+  return hipGetLastError();
 }
 
 hipError_t edge_gemm_init() {

@@ -52,7 +52,9 @@ struct chm_model {
   void* mem2 = nullptr;  // fp16 planes + scales arena
   int math = MATH_SPLIT16;
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
-  int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
+  int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
+  int edge_stagger = 0;
+  const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge layer 1 launch's block timeline  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   std::vector<LayerW> layers;
 };
 
@@ -209,6 +211,9 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->math = mode == "f32" ? MATH_F32 : mode == "bf16x3" ? MATH_BF16X3 : MATH_SPLIT16;
     const char* dbg = getenv("CHM_EDGE_DBG");
     m->edge_dbg = dbg ? atoi(dbg) : 0;
+    const char* pp = getenv("CHM_EDGE1_PP");
+    if (pp) m->edge1_pp = atoi(pp);
+    m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
     struct Job { const float* src; size_t n; const void** dst; };
@@ -535,7 +540,29 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.node_off = b->node_off; ea.natoms = b->natoms; ea.n2g = b->n2g;
         ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
-        HIPCHK(edge_gemm(ea, EPI_EDGE, s));
+        static int traced = 0;  // profiling: dump the block timeline of the 4th eager launch
+        hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+        const bool tr = m->edge_trace && traced < 4 && hipStreamIsCapturing(s, &cst) == hipSuccess &&
+                        cst == hipStreamCaptureStatusNone && ++traced == 4;
+        unsigned long long* tbuf = nullptr;
+        const long tblocks = 2 * (E / 128 + 1);
+        if (tr) {
+          HIPCHK(hipMalloc(&tbuf, tblocks * 48));
+          HIPCHK(hipMemsetAsync(tbuf, 0, tblocks * 48, s));
+          ea.trace = tbuf;
+        }
+        HIPCHK(m->edge1_pp ? edge_gemm_pp(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s));
+        if (tr) {
+          std::vector<unsigned long long> h(tblocks * 6);
+          HIPCHK(hipStreamSynchronize(s));
+          HIPCHK(hipMemcpy(h.data(), tbuf, tblocks * 48, hipMemcpyDeviceToHost));
+          FILE* f = fopen(m->edge_trace, "wb");
+          if (f) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+          }
+          HIPCHK(hipFree(tbuf));
+        }
       }
       {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
         EdgeArgs ea;
