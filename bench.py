@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
                    "captured HIP graph of the reverse step")
+    p.add_argument("--lanes", type=int, default=1, help="concurrent sample groups per GPU, each on its own stream "
+                   "inside the captured step graph (their GEMM epilogues then overlap each other's matrix work)")
     p.add_argument("--math", choices=["split16", "bf16x3", "f32"], default="split16",
                    help="decoder GEMM arithmetic (both fp32-accurate; see include/chemeleon_hip.h)")
     return p.parse_args()
@@ -174,7 +176,7 @@ def main():
     model.decoder.set_math(args.math)
     it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
                              null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
-                             graph=not args.no_graph)
+                             graph=not args.no_graph, lanes=args.lanes)
     next(it)  # initial state
     # per-kernel HIP-event instrumentation (eager launches only; graph captures are not instrumented)
     _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
@@ -273,7 +275,7 @@ def main():
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
                    "n_samples": total, "n_atoms": args.n_atoms, "timesteps": T_STEPS,
                    "parallelism": f"sample-sharded x{world}", "noise": "philox (device)",
-                   "launch": "eager" if args.no_graph else "hip graph replay per step"},
+                   "launch": "eager" if args.no_graph else f"hip graph replay per step, {args.lanes} stream lane(s)"},
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),

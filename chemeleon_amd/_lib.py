@@ -92,11 +92,11 @@ def check(rc: int, what: str):
         raise RuntimeError(f"{what} failed (code {rc}): {msg}")
 
 
-def ptr(t):
-    """Device pointer of a tensor (or None)."""
+def ptr(t, byte_offset: int = 0):
+    """Device pointer of a tensor (or None), optionally byte_offset bytes into it."""
     if t is None:
         return None
-    return c_void_p(t.data_ptr())
+    return c_void_p(t.data_ptr() + byte_offset)
 
 
 def stream_handle(device=None):

@@ -78,6 +78,10 @@ hipError_t gemm_bf16x3(const GemmArgs& g, int epi, hipStream_t s);
 // 256x256-tile variant (edge GEMMs); EPI_SEGMEAN tiles must then hold <= 256 rows
 hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s);
 hipError_t gemm_init();  // one-time kernel attributes (call outside stream capture)
+// node GEMMs, bf16x3 with global_load_lds staging (node_gemm.hip); EPI_STD semantics of gemm_bf16x3
+hipError_t node_gemm(const GemmArgs& g, hipStream_t s);
+hipError_t node_gemm_init();
+extern int g_node_variant;  // microbenchmark probes of node_gemm (0 in the product)
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)

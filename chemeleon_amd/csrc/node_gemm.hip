@@ -1,0 +1,218 @@
+// Node GEMMs of the decoder (FiLM projection, per-node halves of edge layer 1, node MLP, heads,
+// conditioning; cspnet.py:78-97, 150-181, 396-403) in fp32-accurate "bf16x3" arithmetic:
+// C[M,N] = epi(A[M,K] . W[N,K]^T), A fp32, W pre-split into three bf16 planes [3][N][K].
+//
+// Both operands are staged global -> LDS with global_load_lds (no VGPR round trip, no LDS stores
+// from registers): A as raw fp32, W as its three planes. Each wave then splits its own A
+// fragments (8 fp32 per lane and k-step) into three bf16 parts in registers right before the
+// six MFMA products (a2w0 + a1w1 + a0w2 + a1w0 + a0w1 + a0w0, small terms first), so the split
+// costs ~100 VALU per 24 MFMAs instead of an LDS round trip of three planes per block.
+//
+// 128x128 tiles, 256 threads (4 waves of 64x64, C^T accumulators as in gemm_bf16x3.hip),
+// K-tiles of 16, a 4-deep ring of 20 KB stages (3 K-tiles in flight), two blocks per CU.
+// LDS image per stage: A [128 rows][4 pieces of 4 fp32], piece p of row r at p ^ ((r >> 2) & 3);
+// W plane q [128 rows][2 pieces of 8 bf16], piece p of row r at p ^ ((r >> 3) & 1): the
+// fragment reads of every 16-lane group then cover all 64 banks.
+#include "chm_internal.h"
+
+namespace chm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+namespace {
+
+constexpr int NM = 128, NN = 128, NK = 16;
+constexpr int A_ROWB = NK * 4, W_ROWB = NK * 2;  // 64 B, 32 B
+constexpr int A_STB = NM * A_ROWB;               // 8 KB
+constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
+constexpr int STB = A_STB + 3 * W_PLB;           // 20 KB
+constexpr int NST = 4;
+constexpr int NODE_LDS = NST * STB;              // 80 KB: two blocks per CU
+
+__device__ __forceinline__ float silu_n(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+
+__device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);
+}
+
+}  // namespace
+
+// VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
+template <int VAR>
+__global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int ntn = g.N / NN;
+  const long bid = blockIdx.x;
+  const int n0 = (int)(bid % ntn) * NN;
+  const long row0 = (bid / ntn) * NM;
+  const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
+  const int nk = g.K / NK;
+
+  // ---- glds sources. A: instruction q (of 8) covers rows 16q + (L >> 2), LDS piece L & 3 holding
+  // logical piece (L & 3) ^ ((L >> 4) & 3); wave w issues q = 2w, 2w + 1.
+  // W: instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1 holding
+  // logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
+  const int alp = (lane & 3) ^ ((lane >> 4) & 3);
+  const float* asrc[2];
+  const float* asrc2[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = 16 * (2 * wave + u) + (lane >> 2);
+    const long ar = row0 + (r < nrows ? r : nrows - 1);
+    asrc[u] = g.A + ar * g.lda + 4 * alp;
+    asrc2[u] = g.A2 + ar * g.lda2 + 4 * alp - g.ksplit;
+  }
+  const int wlp = (lane & 1) ^ ((lane >> 4) & 1);
+  const __bf16* Wpl = reinterpret_cast<const __bf16*>(g.Wp3);
+  const long wplane = (long)g.N * g.K;
+  const __bf16* wsrc[3];
+  int wdst[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int q = 3 * wave + u, p = q >> 2, rq = q & 3;
+    wsrc[u] = Wpl + p * wplane + (long)(n0 + 32 * rq + (lane >> 1)) * g.K + 8 * wlp;
+    wdst[u] = A_STB + p * W_PLB + 32 * rq * W_ROWB;
+  }
+  auto issue = [&](int t) {
+    const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
+    char* st = lds + (t % NST) * STB;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (2 * wave + u) * A_ROWB), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + k0), (lds_void*)(st + wdst[u]), 16, 0, 0);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // fragment offsets: A row wm*64 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
+  const int asw = (r32 >> 2) & 3, wsw = (r32 >> 3) & 1;
+  const int fa0 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
+  const int fa1 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
+  const int fw = A_STB + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
+
+  issue(0);
+  issue(1);
+  issue(2);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // this thread's part of tile t has landed
+    __builtin_amdgcn_s_barrier();                      // everyone's; everyone is done with tile t-1
+    asm volatile("" ::: "memory");
+    issue(t + 3);
+    const char* st = lds + (t % NST) * STB;
+    f32x4 a0[2], a1[2];
+    bf16x8 w[3][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
+      a1[i] = *reinterpret_cast<const f32x4*>(st + fa1 + i * 32 * A_ROWB);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w[p][j] = *reinterpret_cast<const bf16x8*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
+    bf16x8 a[3][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 x0, x1, x2;
+        if (VAR == 1) {
+          x0 = x1 = x2 = (__bf16)(e < 4 ? a0[i][e] : a1[i][e - 4]);
+        } else {
+          split3n(e < 4 ? a0[i][e] : a1[i][e - 4], x0, x1, x2);
+        }
+        a[0][i][e] = x0;
+        a[1][i][e] = x1;
+        a[2][i][e] = x2;
+      }
+    // small terms first, the leading product last (as gemm_bf16x3.hip)
+    constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+    constexpr int PW[6] = {0, 1, 2, 0, 1, 0};
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[PW[k]][j], a[PA[k]][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the block exits
+
+  // lane l owns output row wm*64 + 32i + (l & 31) and, per 4-register group q, the four
+  // consecutive columns wn*64 + 32j + 8q + 4h .. +3
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 64 + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+    const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+        if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+        if (g.act == 1)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
+        if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+        *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+      }
+  }
+}
+
+int g_node_variant = 0;
+
+hipError_t node_gemm_init() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_node_gemm<0>, hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_node_gemm<1>, hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
+  return e;
+}
+
+hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
+  if (g.M <= 0 || g.N % NN || g.K % NK || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
+  if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = node_gemm_init();
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long blocks = ((g.M + NM - 1) / NM) * (g.N / NN);
+  if (g_node_variant == 1)
+    hipLaunchKernelGGL(k_node_gemm<1>, dim3((unsigned)blocks), dim3(256), NODE_LDS, s, g);
+  else
+    hipLaunchKernelGGL(k_node_gemm<0>, dim3((unsigned)blocks), dim3(256), NODE_LDS, s, g);
+  return hipGetLastError();
+}
+
+}  // namespace chm

@@ -52,6 +52,7 @@ struct chm_model {
   void* mem2 = nullptr;  // fp16 planes + scales arena
   int math = MATH_SPLIT16;
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
+  int node_glds = 0;     // CHM_NODE_GLDS=1: node GEMMs on the glds-staged kernel (node_gemm.hip; measured equal)
   int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
   int edge_stagger = 0;
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge layer 1 launch's block timeline  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
@@ -107,6 +108,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   {
     hipError_t e0 = gemm_init();
     if (e0 == hipSuccess) e0 = edge_gemm_init();
+    if (e0 == hipSuccess) e0 = node_gemm_init();
     if (e0 != hipSuccess) return fail(CHM_E_HIP, std::string("gemm_init: ") + hipGetErrorString(e0));
   }
 
@@ -211,6 +213,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->math = mode == "f32" ? MATH_F32 : mode == "bf16x3" ? MATH_BF16X3 : MATH_SPLIT16;
     const char* dbg = getenv("CHM_EDGE_DBG");
     m->edge_dbg = dbg ? atoi(dbg) : 0;
+    const char* ng = getenv("CHM_NODE_GLDS");
+    if (ng) m->node_glds = atoi(ng);
     const char* pp = getenv("CHM_EDGE1_PP");
     if (pp) m->edge1_pp = atoi(pp);
     m->edge_trace = getenv("CHM_EDGE_TRACE");
@@ -483,6 +487,7 @@ static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const floa
 static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
   if (b->math == MATH_F32) return gemm(g, epi, s);
   g.Wp3 = W3;
+  if (epi == EPI_STD && b->m->node_glds) return node_gemm(g, s);
   return gemm_bf16x3(g, epi, s);
 }
 

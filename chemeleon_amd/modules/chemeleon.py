@@ -178,14 +178,22 @@ class Chemeleon(nn.Module):
                       text_embeds=None, null_text_embeds=None, clone: bool = True, t_stop: int = 0,
                       node_base: int = 0, graph_base: int = 0,
                       init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                      graph: bool = False) -> Iterator[Tuple]:
+                      graph: bool = False, lanes: int = 1) -> Iterator[Tuple]:
         """Reverse loop of chemeleon.py:305-467 yielding device tensors
         (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
         starting with the pure-noise state at t = T.
 
         graph=True (noise="philox" only): one reverse step is captured once
         as a HIP graph (chm_sample_step_dt reads t from device memory and
-        decrements it) and replayed for every timestep."""
+        decrements it) and replayed for every timestep.
+
+        lanes > 1 (graph mode): the crystals are split into that many contiguous
+        groups of similar edge work, each stepped on its own stream inside the
+        one captured graph. The groups' kernels then run concurrently, so one
+        group's GEMM epilogues (store bursts, VALU) overlap the other's matrix
+        work instead of every CU reaching its epilogue at the same moment.
+        Results are bit-identical: Philox noise is keyed by global node / graph
+        index and crystals never interact."""
         if isinstance(natoms, int):
             natoms = [natoms]
         natoms = [int(n) for n in natoms]
@@ -224,16 +232,35 @@ class Chemeleon(nn.Module):
         if graph:
             if noise != "philox":
                 raise ValueError("graph=True needs noise='philox' (host noise cannot be replayed)")
-            d_t = torch.full((1,), T, dtype=torch.int32, device=dev)
+            from ..distributed import partition
+            groups = partition(natoms, max(1, min(int(lanes), B)))
+            d_t = torch.full((len(groups),), T, dtype=torch.int32, device=dev)
+            noff = [0]
+            for n in natoms:
+                noff.append(noff[-1] + n)
+            # per-lane workspaces are created before the capture (allocation is not capturable)
+            lane_batches = [batch if len(groups) == 1 else self.decoder.hip_batch(natoms[g0:g1], max_pairs=2)
+                            for g0, g1 in groups]
             hg = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
+            lane_streams = [torch.cuda.Stream(device=dev) for _ in groups[1:]]
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 with torch.cuda.graph(hg, stream=side):
-                    _lib.check(L.chm_sample_step_dt(batch.handle, sched, _lib.ptr(d_t), float(cond_scale),
-                                                    _lib.ptr(a), _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond),
-                                                    _lib.ptr(null), seed, node_base, graph_base,
-                                                    _lib.stream_handle(dev)), "chm_sample_step_dt")
+                    for k, (g0, g1) in enumerate(groups):
+                        st = side if k == 0 else lane_streams[k - 1]
+                        if k > 0:
+                            st.wait_stream(side)
+                        n0 = noff[g0]
+                        bk = lane_batches[k]
+                        tx = cond.shape[1] * 4 * g0 if cond is not None else 0
+                        with torch.cuda.stream(st):
+                            _lib.check(L.chm_sample_step_dt(
+                                bk.handle, sched, _lib.ptr(d_t, 4 * k), float(cond_scale), _lib.ptr(a, 8 * n0),
+                                _lib.ptr(x, 12 * n0), _lib.ptr(lat, 36 * g0), _lib.ptr(cond, tx), _lib.ptr(null, tx),
+                                seed, node_base + n0, graph_base + g0, _lib.stream_handle(dev)), "chm_sample_step_dt")
+                    for st in lane_streams:
+                        side.wait_stream(st)
             torch.cuda.current_stream(dev).wait_stream(side)
             d_t.fill_(T)
             for t in range(T, t_stop, -1):

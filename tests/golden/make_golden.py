@@ -384,13 +384,25 @@ def gen_trajectory(chm, csp, T=100, every=1):
          final_sorted_scaled=order_scaled, weights_crc=weights_crc(sd), t=ts, **extra)
 
 
+def gen_state_keys(chm, csp):
+    """Names and shapes of the reference Chemeleon state_dict (decoder, schedulers, D3PM): the
+    layout a Lightning checkpoint of the reference carries under `state_dict`."""
+    import json
+    m, _ = build_reference_model(chm, csp, 1000)
+    keys = {k: list(v.shape) for k, v in m.state_dict().items() if not k.startswith("text_encoder.")}
+    path = os.path.join(HERE, "state_keys.json")
+    with open(path, "w") as f:
+        json.dump(keys, f, indent=0, sort_keys=True)
+    print("wrote", path, len(keys), "keys")
+
+
 if __name__ == "__main__":
     if not os.path.isdir(os.path.join(REF, "chemeleon")):
         print("reference not present; nothing to do")
         sys.exit(0)
     torch.set_num_threads(8)
     chm, csp, du, sc = load_reference()
-    which = sys.argv[1:] or ["schedules", "units", "decoder", "steps", "trajectory"]
+    which = sys.argv[1:] or ["schedules", "units", "decoder", "steps", "trajectory", "keys"]
     if "schedules" in which:
         gen_schedules(chm, csp)
     if "units" in which:
@@ -401,5 +413,7 @@ if __name__ == "__main__":
         gen_single_steps(chm, csp)
     if "trajectory" in which:
         gen_trajectory(chm, csp)
+    if "keys" in which:
+        gen_state_keys(chm, csp)
     if "trajectory1000" in which:
         gen_trajectory(chm, csp, T=1000, every=10)

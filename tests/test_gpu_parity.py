@@ -329,14 +329,17 @@ def test_philox_shard_invariance(model100, cn):
         assert torch.equal(cat, full[k]), f"state {k} differs between 1 and 2 shards"
 
 
-def test_graph_replay_matches_eager(model100, cn):
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_graph_replay_matches_eager(model100, cn, lanes):
     """One captured reverse step replayed per timestep (device-side t) gives
-    bit-identical states to eager stepping."""
-    nat = [5, 9, 3, 12]
+    bit-identical states to eager stepping, also with the crystals split over
+    concurrent stream lanes inside the graph."""
+    nat = [5, 9, 3, 12, 7, 1, 20]
     runs = []
     for graph in (False, True):
         states = list(model100.sample_states(nat, None, 2.0, 1e-5, noise="philox", seed=11, text_embeds=cn[0],
-                                             null_text_embeds=cn[1], clone=True, graph=graph, t_stop=80))
+                                             null_text_embeds=cn[1], clone=True, graph=graph, t_stop=80,
+                                             lanes=lanes))
         runs.append(states)
     assert [s[0] for s in runs[0]] == [s[0] for s in runs[1]]
     for se, sg in zip(*runs):

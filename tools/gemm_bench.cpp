@@ -139,6 +139,30 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
+    CK(node_gemm_init());
+    for (int rep = 0; rep < 2; ++rep) {
+      g_gemm3_variant = 0;
+      float tr = time_it(10, s, [&] { CK(gemm_bf16x3(g, EPI_STD, s)); });
+      float tn = time_it(10, s, [&] { CK(node_gemm(g, s)); });
+      GemmArgs g0 = g; g0.bias = nullptr; g0.act = 0;
+      float tn0 = time_it(10, s, [&] { CK(node_gemm(g0, s)); });
+      g_node_variant = 1;
+      float tv = time_it(10, s, [&] { CK(node_gemm(g0, s)); });
+      g_node_variant = 0;
+      printf("M=%ld N=%d K=%d  k_gemm3 %.1f us %.1f TF | k_node_gemm %.1f us %.1f TF (no bias/act %.1f us, no split %.1f us)\n",
+             M, N, K, tr * 1e3, flops / tr / 1e9, tn * 1e3, flops / tn / 1e9, tn0 * 1e3, tv * 1e3);
+    }
+    std::vector<float> c1(65536), c2(65536);
+    CK(gemm_bf16x3(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
+    CK(node_gemm(g, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0;
+    for (size_t i = 0; i < c1.size(); ++i) mx = fmax(mx, fabs((double)c1[i] - c2[i]));
+    printf("  max |node - gemm3| = %.3e\n", mx);
+    return 0;
+  }
   float t32 = time_it(5, s, [&] { CK(gemm(g, EPI_STD, s)); });
   printf("M=%ld N=%d K=%d  f32-mfma: %.3f ms %.1f TF\n", M, N, K, t32, flops / t32 / 1e9);
   for (int v = 0; v < 4; ++v) {

@@ -45,3 +45,12 @@ k0 = sorted(cu)[0]
 for k in sorted(cu)[:3]:
     idx = sorted(cu[k], key=lambda i: t0[i])
     print(f"CU {k:#x}: " + " ".join(f"[{t0[i] / 100:.0f} {tm[i] / 100:.0f} {te[i] / 100:.0f}]" for i in idx[:8]))
+# concurrency: fraction of CUs in their epilogue over time (10 us bins)
+span = int(te.max())
+bins = np.zeros(span // 1000 + 1)
+for i in range(len(a)):
+    lo, hi = int(tm[i]) // 1000, int(te[i]) // 1000
+    bins[lo:hi + 1] += 1
+frac = bins / len(cu)
+print("CUs in epilogue per 10 us bin (first 40):", " ".join(f"{f:.2f}" for f in frac[:40]))
+print(f"epilogue concurrency: mean {frac.mean():.2f}, p10 {np.percentile(frac, 10):.2f}, p90 {np.percentile(frac, 90):.2f}")
