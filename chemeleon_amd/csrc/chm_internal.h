@@ -42,7 +42,7 @@ enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 struct EdgeArgs {
   long M;
   int N, K;
-  const void* A;                  // split rows [rows][K/32][2][32] fp16
+  const void* A;                  // split rows [rows][K/32][2][32] fp16, readable 256 rows past the last
   const int* aexp;               // per A row: 4 packed int8 exponents of its 128-column chunks, or null
   const void* W;                 // split rows [N][K/32][2][32], rows scaled by 1 / wscale
   const float* wscale;

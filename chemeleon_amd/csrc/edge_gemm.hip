@@ -244,7 +244,7 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
 template <int EPI, bool ASC, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
   const int ntn = g.N / BN;
@@ -289,10 +289,9 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   // swz(r + 8q) = ((r >> 1) + 4q) & 7 = swz(r) ^ 4 (q & 1): the chunk offset alternates with q
   const unsigned lc16 = 16u * (unsigned)((lane & 7) ^ ((lr0 >> 1) & 7));
   const unsigned lc16x = lc16 ^ 64u;
-  // (the per-row A offsets are recomputed at each issue: hoisted, they cost 4 VGPRs the
-  // main loop does not have)
-  int lr0v = lr0;
-  unsigned lcv = lc16;
+  // A rows past the tile's nrows are read unclamped: the A buffers (F, S) carry 256 rows of
+  // padding, and those rows' accumulators are never stored. A and W then share one set of
+  // per-lane offsets (no per-issue clamp arithmetic in the loop).
   const unsigned woff = (unsigned)(lr0 * rowB) + lc16;
   const unsigned wq = (unsigned)(8 * rowB);
   char* dst = lds + wave * 32 * ROW_B;
@@ -300,13 +299,10 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   auto issueA = [&](int t) {
     const char* src = Ablk + (long)(t < nk ? t : nk - 1) * ROW_B;
     char* d = dst + (t % NSA) * OPND_B;
-    asm volatile("" : "+v"(lr0v), "+v"(lcv));  // keep the offsets from being hoisted
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = lr0v + q * 8;
-      const unsigned off = (unsigned)((r < nrows ? r : (int)nrows - 1) * (int)rowB) + ((q & 1) ? (lcv ^ 64u) : lcv);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + off), (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
-    }
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq + ((q & 1) ? (lc16x - lc16) : 0u))),
+                                       (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
   };
   auto issueW = [&](int t) {
     const char* src = Wblk + (long)(t < nk ? t : nk - 1) * ROW_B;

@@ -381,8 +381,9 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->agg = fl((size_t)P * N * H);
   b->PQ = fl((size_t)P * N * 2 * H);
   b->gbias = fl((size_t)L * B * H);
-  b->F = fl((size_t)E * FD);
-  b->S = fl((size_t)P * E * H);
+  // (F and S carry kTileRows rows of padding: the split16 edge GEMMs read whole 256-row tiles)
+  b->F = fl((size_t)(E + kTileRows) * FD);
+  b->S = fl(((size_t)P * E + kTileRows) * H);
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
   b->Hf = fl((size_t)P * N * H);
