@@ -52,7 +52,7 @@ struct chm_model {
   void* mem2 = nullptr;  // fp16 planes + scales arena
   int math = MATH_SPLIT16;
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
-  int node_glds = 0;     // CHM_NODE_GLDS=1: node GEMMs on the glds-staged kernel (node_gemm.hip; measured equal)
+  int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
   int edge_stagger = 0;
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge layer 1 launch's block timeline  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
