@@ -394,46 +394,91 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   read_frags(0, 0, 0);
   for (int t = 0; t < nk; ++t) {
     __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): set 0 (read under the last MFMAs) is in
-    if (VAR == 0 || VAR == 3) {
+    if (VAR == 0 || VAR == 3 || VAR >= 5) {
       // explicit interleave: each fragment read / load issue sits between two MFMAs (+7.5% over
       // the compiler's schedule, which clusters the 8 load issues and 12 reads ahead of the MFMAs;
       // VAR 4 keeps that schedule for comparison)
       rescale(t);
-      __builtin_amdgcn_s_setprio(1);
+      if (VAR != 7) __builtin_amdgcn_s_setprio(1);
       read_frags(1, t, 1);
       mfma_group(0, 1, 0);
       mfma_group(0, 0, 1);
       mfma_group(0, 0, 0);
+      if (VAR != 3) {  // reads spread one per two MFMAs (VAR 3: the first twelve MFMAs)
 #pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-      __builtin_amdgcn_s_setprio(0);
+      if (VAR != 7) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_s_waitcnt(0xC07F);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
+      if (VAR != 7) __builtin_amdgcn_s_setprio(1);
       issueW(t + 2);
       issueA(t + 3);
       read_frags(0, t + 1, 0);
       mfma_group(1, 1, 0);
       mfma_group(1, 0, 1);
       mfma_group(1, 0, 0);
+      if (VAR == 6) {  // (microbenchmark) load issues first, then reads between MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x010, 8, 1);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
-      }
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 1);
+      } else if (VAR == 5) {  // (microbenchmark) load issues and reads mixed 2 : 3 between MFMAs
 #pragma unroll
-      for (int k = 0; k < 12; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+      } else if (VAR == 8) {  // (microbenchmark) reads first (they feed the next tile), loads later
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+        }
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
-      __builtin_amdgcn_s_setprio(0);
+      if (VAR != 7) __builtin_amdgcn_s_setprio(0);
       continue;
     }
     read_frags(1, t, 1);
@@ -799,8 +844,12 @@ hipError_t edge_gemm_init() {
 }
 
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s) {
-  const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false, 1>, (const void*)k_edge_gemm<EPI_STD, false, 2>,
-                      (const void*)k_edge_gemm<EPI_STD, false, 3>, (const void*)k_edge_gemm<EPI_STD, false, 4>};
+  const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false, 0>, (const void*)k_edge_gemm<EPI_STD, false, 1>,
+                      (const void*)k_edge_gemm<EPI_STD, false, 2>, (const void*)k_edge_gemm<EPI_STD, false, 3>,
+                      (const void*)k_edge_gemm<EPI_STD, false, 4>, (const void*)k_edge_gemm<EPI_STD, false, 5>,
+                      (const void*)k_edge_gemm<EPI_STD, false, 6>, (const void*)k_edge_gemm<EPI_STD, false, 7>,
+                      (const void*)k_edge_gemm<EPI_STD, false, 8>};
+  if (var < 0 || var > 8) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     for (const void* k : ks) {
@@ -810,17 +859,9 @@ hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s) {
     attr = true;
   }
   const long blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
-  if (var == 1)
-    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 1>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
-  else if (var == 2)
-    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 2>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
-  else if (var == 3)
-    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 3>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
-  else if (var == 4)
-    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 4>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
-  else
-    hipLaunchKernelGGL((k_edge_gemm<EPI_STD, false, 0>), dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
-  return hipGetLastError();
+  EdgeArgs ga = g;
+  void* args[] = {&ga};
+  return hipLaunchKernel(ks[var], dim3((unsigned)blocks), dim3(512), args, LDS_B, s);
 }
 
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {

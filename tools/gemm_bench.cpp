@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
     }
     ea.C = nullptr;
     for (int rep = 0; rep < 3; ++rep)
-      for (int var = 0; var < 5; ++var) {
+      for (int var : {0, 3, 5, 7}) {
         float tv = time_it(5, s, [&] { CK(edge_gemm_variant(ea, var, s)); });
         printf("  variant %d (no C): %.3f ms %.1f TF\n", var, tv, flops / tv / 1e9);
       }
