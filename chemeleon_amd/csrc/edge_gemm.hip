@@ -51,6 +51,10 @@ constexpr int LDS_B = RING_B > SEG_B + 2048 ? RING_B : SEG_B + 2048;  // (+ the 
 constexpr int CHUNK = 128;                  // S scale granularity (columns)
 constexpr int PQ_PITCH = 260;               // EPI_EDGE staged P / Q rows (floats)
 constexpr int PQ_OFF = 0;
+// P / Q rows staged by the main loop's last iterations (EPI_EDGE, K = 768): conditioning 0 at row 0
+// (A stages 0-1, free after the barrier of K-tile nk-2), conditioning 1 at row PRE_ROW1 (free after
+// the barrier of nk-1); both images hold up to PRE_MAX rows
+constexpr int PRE_ROW1 = 63, PRE_MAX = 61;
 
 __device__ __forceinline__ float silu_e(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
@@ -87,7 +91,7 @@ __device__ __forceinline__ int exp_of(float m) {
 // multiplied by wscale. NW waves, ldsb bytes of free LDS.
 template <int NW>
 __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2][4], char* lds, int ldsb, int wave,
-                                              int lane, long row0, long nrows, int n0) {
+                                              int lane, long row0, long nrows, int n0, bool pre = false) {
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, r32 = lane & 31;
   const int PQ_ROWS = ldsb / (PQ_PITCH * 4);
     // S[c][e] = SiLU(acc + P_c[i] + Q_c[j]) written as hi/lo fp16 planes scaled by 2^-e per
@@ -102,7 +106,8 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
     const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
     const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
     const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1;
-    const bool staged = nP + nQ <= PQ_ROWS;
+    // pre: the main loop already staged both conditionings (rows [0, nR) and [PRE_ROW1, ...))
+    const bool staged = pre || nP + nQ <= PQ_ROWS;
     const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
     long rowv[2];
     int pr[2], qr[2];  // staged: LDS rows; gathered: node indices
@@ -122,9 +127,9 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
     // waited on would wait for those stores to drain: when both conditionings' rows fit, they are
     // staged together before any store (rows [c * nR, (c + 1) * nR)).
     const int nR = nP + nQ;
-    const bool both = staged && g.npairs * nR <= PQ_ROWS;
+    const bool both = pre || (staged && g.npairs * nR <= PQ_ROWS);
     auto stage = [&](int c0, int c1) {  // conditionings [c0, c1)
-      if (!staged) return;
+      if (!staged || pre) return;
       if (c0 > 0) __syncthreads();  // everyone is done reading the previous conditioning
       for (int c = c0; c < c1; ++c) {
         const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
@@ -145,7 +150,7 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
     auto run = [&](int c, auto LAST, auto STG) {
       constexpr bool last = decltype(LAST)::value, stg = decltype(STG)::value;
       const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-      const int rb = both ? c * nR : 0;
+      const int rb = pre ? c * PRE_ROW1 : (both ? c * nR : 0);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const long lr = wm * 64 + i * 32 + r32;  // rows past nrows compute clamped copies, never stored
@@ -392,7 +397,31 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read_frags(0, 0, 0);
-  for (int t = 0; t < nk; ++t) {
+  // EPI_EDGE: stage the epilogue's P / Q rows during the last two K-tiles (their latency then hides
+  // under those MFMAs) when the ring layout allows (nk % 6 == 0) and the rows fit (nR <= PRE_MAX)
+  bool pre = false;
+  int p_ilo = 0, p_jlo = 0, p_nP = 0, p_nR = 0;
+  if constexpr (EPI == EPI_EDGE) {
+    if (nk % 6 == 0 && !(g.dbg & 2048)) {
+      const long rl = row0 + nrows - 1;
+      p_ilo = g.ei[row0];
+      const int ihi = g.ei[rl], ghi = g.n2g[ihi];
+      p_jlo = g.node_off[g.n2g[p_ilo]];
+      p_nP = ihi - p_ilo + 1;
+      p_nR = p_nP + g.node_off[ghi] + g.natoms[ghi] - p_jlo;
+      pre = p_nR <= PRE_MAX;
+    }
+  }
+  auto stage_rows = [&](int c, int rbase) {
+    const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+    for (int r = wave; r < p_nR; r += 8) {
+      const float* src = Pc + (r < p_nP ? (long)(p_ilo + r) * (2 * H) : (long)(p_jlo + r - p_nP) * (2 * H) + H) + n0 +
+                         4 * lane;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + (rbase + r) * PQ_PITCH * 4), 16, 0, 0);
+    }
+  };
+  const int nmain = pre ? nk - 3 : nk;
+  for (int t = 0; t < nmain; ++t) {
     __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): set 0 (read under the last MFMAs) is in
     if (VAR == 0 || VAR == 3 || VAR >= 5) {
       // explicit interleave: each fragment read / load issue sits between two MFMAs (+7.5% over
@@ -508,6 +537,23 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     read_frags(0, t + 1, 0);                           // past the end: reads a re-read tile
     mfmas(1);
   }
+  // EPI_EDGE with pre-staging: the last three K-tiles, without the tail re-reads (their stages
+  // receive the P / Q images instead)
+  for (int t = nk - 3; pre && t < nk; ++t) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    read_frags(1, t, 1);
+    mfmas(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                 // this wave is done reading tile t
+    if (t == nk - 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile nk-2 (A nk-1 in flight)
+    if (t == nk - 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile nk-1
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t == nk - 3) issueW(t + 2);
+    if (t == nk - 2) stage_rows(0, 0);
+    if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
+    if (t < nk - 1) read_frags(0, t + 1, 0);
+    mfmas(1);
+  }
   // drain the ring (the tail re-reads still land in LDS) before the epilogue reuses it
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -605,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
 
   if (EPI == EPI_EDGE) {
     const unsigned long long tm = g.trace ? rtime() : 0;
-    edge_epilogue<8>(g, acc, lds, LDS_B, wave, lane, row0, nrows, n0);
+    edge_epilogue<8>(g, acc, lds, LDS_B, wave, lane, row0, nrows, n0, pre);
     if (g.trace) {
       __syncthreads();
       if (tid == 0) {
