@@ -537,11 +537,12 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     read_frags(0, t + 1, 0);                           // past the end: reads a re-read tile
     mfmas(1);
   }
-  // EPI_EDGE with pre-staging: the last three K-tiles, without the tail re-reads (their stages
-  // receive the P / Q images instead)
+  // pre-staging: the last three K-tiles, without the tail re-reads (their stages receive the
+  // epilogue's data instead)
   for (int t = nk - 3; pre && t < nk; ++t) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     read_frags(1, t, 1);
+    rescale(t);
     mfmas(0);
     __builtin_amdgcn_s_waitcnt(0xC07F);                 // this wave is done reading tile t
     if (t == nk - 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile nk-2 (A nk-1 in flight)
@@ -549,8 +550,11 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t == nk - 3) issueW(t + 2);
-    if (t == nk - 2) stage_rows(0, 0);
-    if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
+    if constexpr (EPI == EPI_EDGE) {
+      if (t == nk - 2) stage_rows(0, 0);
+      if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
+    }
+
     if (t < nk - 1) read_frags(0, t + 1, 0);
     mfmas(1);
   }
@@ -585,6 +589,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     // The tile's node list (atom count, first row) is fetched while the first pass computes and
     // kept in LDS after the tile (int2 [<= 256]).
     if (g.dbg & 128) return;  // (profiling: main loop only)
+    const unsigned long long tm = g.trace ? rtime() : 0;
     float* T = reinterpret_cast<float*>(lds);
     int2* info = reinterpret_cast<int2*>(lds + SEG_B);
     const long es0 = g.node_estart[seg.x];
@@ -645,6 +650,10 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
           g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = sacc / (float)(ni.x < 1 ? 1 : ni.x);
       }
       __syncthreads();
+    }
+    if (g.trace && tid == 0) {
+      unsigned long long* o = g.trace + 6 * blockIdx.x;
+      o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
     }
     return;
   }

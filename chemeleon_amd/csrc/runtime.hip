@@ -54,8 +54,9 @@ struct chm_model {
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
-  int edge_stagger = 0;
-  const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge layer 1 launch's block timeline  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
+  int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
+  const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
+  int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
   std::vector<LayerW> layers;
 };
 
@@ -218,6 +219,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     const char* pp = getenv("CHM_EDGE1_PP");
     if (pp) m->edge1_pp = atoi(pp);
     m->edge_trace = getenv("CHM_EDGE_TRACE");
+    const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
+    if (tl) m->edge_trace_layer = atoi(tl);
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
     struct Job { const float* src; size_t n; const void** dst; };
@@ -499,6 +502,37 @@ static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const v
   return gemm_bf16x3_big(g, epi, s);
 }
 
+// profiling (CHM_EDGE_TRACE=file, CHM_EDGE_TRACE_LAYER=1|2): the 4th eager launch of edge layer
+// 1 or 2 records {hw id, t0, t_mainloop, t_end, ...} per block (s_memrealtime), dumped to the file
+template <class F>
+static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which, long E, hipStream_t s, F&& launch) {
+  static int traced = 0;
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  const bool tr = m->edge_trace && m->edge_trace_layer == which && traced < 4 &&
+                  hipStreamIsCapturing(s, &cst) == hipSuccess && cst == hipStreamCaptureStatusNone && ++traced == 4;
+  if (!tr) return launch();
+  unsigned long long* tbuf = nullptr;
+  const long tblocks = 4 * (E / 128 + 1) + 4096;
+  hipError_t e = hipMalloc(&tbuf, tblocks * 48);
+  if (e == hipSuccess) e = hipMemsetAsync(tbuf, 0, tblocks * 48, s);
+  if (e != hipSuccess) return e;
+  ea.trace = tbuf;
+  e = launch();
+  ea.trace = nullptr;
+  std::vector<unsigned long long> h(tblocks * 6);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipMemcpy(h.data(), tbuf, tblocks * 48, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) {
+    FILE* f = fopen(m->edge_trace, "wb");
+    if (f) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
+  hipFree(tbuf);
+  return e;
+}
+
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
                        int tstride, const int* d_t, const float* text0, const float* text1, int heads,
@@ -546,29 +580,9 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.node_off = b->node_off; ea.natoms = b->natoms; ea.n2g = b->n2g;
         ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
-        static int traced = 0;  // profiling: dump the block timeline of the 4th eager launch
-        hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
-        const bool tr = m->edge_trace && traced < 4 && hipStreamIsCapturing(s, &cst) == hipSuccess &&
-                        cst == hipStreamCaptureStatusNone && ++traced == 4;
-        unsigned long long* tbuf = nullptr;
-        const long tblocks = 2 * (E / 128 + 1);
-        if (tr) {
-          HIPCHK(hipMalloc(&tbuf, tblocks * 48));
-          HIPCHK(hipMemsetAsync(tbuf, 0, tblocks * 48, s));
-          ea.trace = tbuf;
-        }
-        HIPCHK(m->edge1_pp ? edge_gemm_pp(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s));
-        if (tr) {
-          std::vector<unsigned long long> h(tblocks * 6);
-          HIPCHK(hipStreamSynchronize(s));
-          HIPCHK(hipMemcpy(h.data(), tbuf, tblocks * 48, hipMemcpyDeviceToHost));
-          FILE* f = fopen(m->edge_trace, "wb");
-          if (f) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-          }
-          HIPCHK(hipFree(tbuf));
-        }
+        HIPCHK(traced_edge_launch(m, ea, 1, E, s, [&] {
+          return m->edge1_pp ? edge_gemm_pp(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s);
+        }));
       }
       {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
         EdgeArgs ea;
@@ -578,7 +592,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
         ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-        HIPCHK(edge_gemm(ea, EPI_SEGMEAN, s));
+        HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] { return edge_gemm(ea, EPI_SEGMEAN, s); }));
       }
     } else {
       {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
