@@ -57,6 +57,7 @@ struct EdgeArgs {
   const int2* tiles; int ntiles;
   const long* node_estart;
   const int* natoms; const int* n2g;
+  const int* node_n;             // EPI_SEGMEAN: atom count of each node's crystal
   float* agg;
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none

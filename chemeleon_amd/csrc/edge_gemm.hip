@@ -562,13 +562,26 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // ---- undo the scales: W rows (columns of the output) and the last A chunk
-  {
-    float rs[2] = {1.0f, 1.0f};
-    if (ASC) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
+  // EPI_SEGMEAN: the tile's node list {atom count, first row in the tile} for thread tid < nodes,
+  // loaded first so its two dependent loads overlap the scale loads and the SiLU below
+  int2 my = {0, 0};
+  if (EPI == EPI_SEGMEAN && !(g.dbg & 128)) {
+    const long es0 = g.node_estart[seg.x];
+    if (tid < seg.y - seg.x) {
+      const int nd = seg.x + tid;
+      my.x = g.node_n[nd];  // independent loads (no n2g -> natoms chain)
+      my.y = (int)(g.node_estart[nd] - es0);
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep them issued here, ahead of the scale undo and SiLU
+  }
+
+  // ---- undo the scales: W rows (columns of the output) and the last A chunk
+  float rs[2] = {1.0f, 1.0f};
+  if (ASC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
+  }
+  if constexpr (EPI != EPI_SEGMEAN) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -586,33 +599,53 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   if (EPI == EPI_SEGMEAN) {
     // two passes of 128 columns: the wn-th half of the waves writes SiLU(acc + b2) to an
     // LDS tile [256][132], then every thread sums node segments of one column in edge order.
-    // The tile's node list (atom count, first row) is fetched while the first pass computes and
-    // kept in LDS after the tile (int2 [<= 256]).
+    // The tile's node list (atom count, first row; loaded before the scale undo) is kept in LDS
+    // after the tile (int2 [<= 256]).
     if (g.dbg & 128) return;  // (profiling: main loop only)
     const unsigned long long tm = g.trace ? rtime() : 0;
     float* T = reinterpret_cast<float*>(lds);
     int2* info = reinterpret_cast<int2*>(lds + SEG_B);
-    const long es0 = g.node_estart[seg.x];
     const int nn = seg.y - seg.x;
-    int2 my = {0, 0};
-    if (tid < nn) {
-      const int nd = seg.x + tid;
-      my.x = g.natoms[g.n2g[nd]];
-      my.y = (int)(g.node_estart[nd] - es0);
-    }
-    // every wave applies bias + SiLU to its accumulators first (all eight waves at once), then the
-    // owners of each 128-column half write it to the tile
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
+    // every wave undoes the scales and applies bias + SiLU to its accumulators first (all eight
+    // waves at once), then the owners of each 128-column half write it to the tile. The scale and
+    // bias vectors are loaded one column group ahead (double-buffered) rather than all up front,
+    // which would spill.
+    f32x4 sc[2][4], bb[2][4];
+    auto ld_sb = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(g.bias + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
+        const int c = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
+        sc[j & 1][q] = *reinterpret_cast<const f32x4*>(g.wscale + c);
+        bb[j & 1][q] = *reinterpret_cast<const f32x4*>(g.bias + c);
+      }
+    };
+    auto act = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr (j < 3) ld_sb(std::integral_constant<int, j + 1>{});
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = silu_e(acc[i][j][4 * q + e] + b[e]);
-      }
+          for (int e = 0; e < 4; ++e)
+            acc[i][j][4 * q + e] = silu_e(acc[i][j][4 * q + e] * (sc[j & 1][q][e] * rs[i]) + bb[j & 1][q][e]);
+      // pin this group's math ahead of the next group's loads (which stay behind the clobber)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          asm volatile("" : "+v"(acc[i][j][4 * q]), "+v"(acc[i][j][4 * q + 1]), "+v"(acc[i][j][4 * q + 2]),
+                       "+v"(acc[i][j][4 * q + 3])::"memory");
+    };
+    ld_sb(std::integral_constant<int, 0>{});
+    act(std::integral_constant<int, 0>{});
+    act(std::integral_constant<int, 1>{});
+    act(std::integral_constant<int, 2>{});
+    act(std::integral_constant<int, 3>{});
+    if (g.trace && tid == 0) g.trace[6 * blockIdx.x + 4] = rtime();  // (profiling) SiLU done
     for (int half = 0; half < 2; ++half) {
+      if (half == 1 && g.trace && tid == 0) g.trace[6 * blockIdx.x + 5] = rtime();  // first half summed
       if (wn == half) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -925,7 +958,7 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
   if (asc && (g.K % CHUNK || g.K / CHUNK > 4)) return hipErrorInvalidValue;
   long blocks;
   if (epi == EPI_SEGMEAN) {
-    if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc) return hipErrorInvalidValue;
+    if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
     blocks = (long)g.ntiles * g.npairs * (g.N / BN);
   } else {
     if (g.M <= 0) return hipErrorInvalidValue;

@@ -68,6 +68,7 @@ struct chm_batch {
   // index tables
   int *natoms, *node_off, *n2g, *ei, *ej;
   long *edge_off, *node_estart;
+  int* node_n;  // atom count of each node's crystal
   int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
   int math;     // arithmetic mode fixed at creation (copied from the model)
@@ -373,9 +374,10 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->ei = (int*)alloc(E * sizeof(int));
   b->ej = (int*)alloc(E * sizeof(int));
   b->node_estart = (long*)alloc(N * sizeof(long));
+  b->node_n = (int*)alloc(N * sizeof(int));
   b->tiles = (int2*)alloc(tiles.size() * sizeof(int2));
   b->ntiles = (int)tiles.size();
-  ok = b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej && b->node_estart && b->tiles;
+  ok = b->node_n && b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej && b->node_estart && b->tiles;
   b->cin = fl((size_t)P * B * (TD + X));
   b->cemb = fl((size_t)P * B * 2 * H);
   b->Hres = fl((size_t)P * N * H);
@@ -404,6 +406,11 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   if (e == hipSuccess) e = hipMemcpy(b->ei, ei.data(), E * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(b->ej, ej.data(), E * sizeof(int), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(b->node_estart, estart.data(), N * sizeof(long), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    std::vector<int> nn(N);
+    for (long i = 0; i < N; ++i) nn[i] = nat[n2g[i]];
+    e = hipMemcpy(b->node_n, nn.data(), N * sizeof(int), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemcpy(b->tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     chm_batch_destroy(b);
@@ -590,6 +597,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
         ea.W = w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles; ea.ntiles = b->ntiles;
         ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
+        ea.node_n = b->node_n;
         ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
         HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] { return edge_gemm(ea, EPI_SEGMEAN, s); }));

@@ -15,8 +15,8 @@ main, epi = (tm - t0) / 100, (te - tm) / 100
 t4, t5 = a[:, 4].astype(np.int64) - base, a[:, 5].astype(np.int64) - base
 ok = a[:, 4] > 0
 if ok.any():
-    print(f"epilogue split (blocks staging both): stage {np.median((t4 - tm)[ok]) / 100:.1f} us, "
-          f"cond 0 {np.median((t5 - t4)[ok]) / 100:.1f} us, cond 1 {np.median((te - t5)[ok]) / 100:.1f} us "
+    print(f"epilogue split (markers 4, 5): tm->4 {np.median((t4 - tm)[ok]) / 100:.1f} us, "
+          f"4->5 {np.median((t5 - t4)[ok]) / 100:.1f} us, 5->end {np.median((te - t5)[ok]) / 100:.1f} us "
           f"({ok.sum()} blocks)")
 print(f"per block: main {np.median(main):.1f} us (p10 {np.percentile(main, 10):.1f}, p90 {np.percentile(main, 90):.1f}), "
       f"epilogue {np.median(epi):.1f} us (p10 {np.percentile(epi, 10):.1f}, p90 {np.percentile(epi, 90):.1f})")
