@@ -27,6 +27,14 @@ struct GemmArgs {
   const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
   // bf16x3 path: W split into three bf16 planes [3][N][K] (hi, mid, lo)
   const void* Wp3;
+  // split16 node GEMMs (node_gemm.hip): Wp3 = fp16 hi/lo rows [N][K/16][hi 16 | lo 16] of W scaled
+  // by wscale[n]^-1 (split_rows_h with 16-column chunks); null wscale = bf16x3 planes
+  const float* wscale;
+  // split16 node GEMMs: per A row, max |A[row, :]| (amax, and amax2 for the A2 columns; float
+  // values, >= 0) sets the row's power-of-two scale; null = unscaled. cmax != null: max |C[row, :]|
+  // of the output (after bias / activation / residual) is atomically max-ed into cmax[row] (float
+  // bits as unsigned), for the next GEMM that reads C.
+  const float* amax; const float* amax2; unsigned* cmax;
   // EPI_SEGMEAN (message GEMM + scatter_mean): row tiles cover whole nodes
   const int2* tiles; int ntiles;          // node ranges [x, y) of one conditioning
   const long* node_estart;                // first edge row of each node
@@ -59,6 +67,7 @@ struct EdgeArgs {
   const int* natoms; const int* n2g;
   const int* node_n;             // EPI_SEGMEAN: atom count of each node's crystal
   float* agg;
+  unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers,
@@ -69,7 +78,8 @@ hipError_t edge_gemm_init();
 // two-workgroups-per-CU variant (128x256 tiles), EPI_STD / EPI_EDGE, unscaled A
 hipError_t edge_gemm_pp(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // microbenchmarks
-hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s);
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
+                        int chunk = 32);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
 
 hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
@@ -90,14 +100,19 @@ extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
 hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* F, hipStream_t s);
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,
                         const int* natoms, long N, long E, int P, hipStream_t s);
-hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s);
+// rmax != null: rmax[row] = max |Hout[row, :]|
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr);
 // d_t != null: the time-embedding row is temb + (*d_t) * TD, shared by all graphs
 hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
                          int text_dim, float* cin, int B, int P, hipStream_t s);
 hipError_t decrement(int* d_t, hipStream_t s);
 hipError_t graph_bias(const float* lat, const float* Wc, long ldwc, const float* b1, float* out, int B, hipStream_t s);
+// rmx != null (split16 node GEMMs): rows of the four row-max arrays [4][rstride] (RMX_*): writes
+// max |Hl[row, :]| to RMX_HL and zeroes RMX_H, RMX_AGG, RMX_U for this layer's atomic maxima
+enum { RMX_H = 0, RMX_HL = 1, RMX_AGG = 2, RMX_U = 3 };
 hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
-                   const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s);
+                   const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s,
+                   float* rmx = nullptr, long rstride = 0);
 hipError_t layer_norm(const float* X, float* Y, long rows, const float* w, const float* b, hipStream_t s);
 hipError_t graph_heads(const float* Hf, const float* Wlat, const float* lat, const int* node_off, const int* natoms,
                        long N, int B, int P, float* lat_out, hipStream_t s);

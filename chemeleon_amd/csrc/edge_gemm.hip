@@ -70,6 +70,11 @@ __device__ __forceinline__ unsigned long long rtime() {
   asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
   return t;
 }
+__device__ __forceinline__ unsigned long long ctime() {  // shader clock counter
+  unsigned long long t;
+  asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
 __device__ __forceinline__ unsigned hwid() {
   unsigned hw, xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -223,9 +228,9 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
       if (g.npairs > 1) {
         if (both) {
           stage(0, 2);
-          if (g.trace && threadIdx.x == 0) g.trace[6 * blockIdx.x + 4] = rtime();
+          if (g.trace && !(g.dbg & 4096) && threadIdx.x == 0) g.trace[6 * blockIdx.x + 4] = rtime();
           run(0, F{}, STG);
-          if (g.trace && threadIdx.x == 0) g.trace[6 * blockIdx.x + 5] = rtime();
+          if (g.trace && !(g.dbg & 4096) && threadIdx.x == 0) g.trace[6 * blockIdx.x + 5] = rtime();
         } else {
           stage(0, 1);
           run(0, F{}, STG);
@@ -272,6 +277,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   }
   const int K = g.K, nk = K / BK;
   const unsigned long long t0 = g.trace ? rtime() : 0;
+  const unsigned long long c0 = (g.trace && (g.dbg & 4096)) ? ctime() : 0;  // (clock probe)
   // Every block of a launch does the same work, so CUs that start together stay in lockstep and
   // their epilogues (S / agg stores, VALU-only) coincide: the store bursts then saturate HBM while
   // no CU computes. Holding back every other CU of the first round by about half a tile
@@ -643,9 +649,9 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     act(std::integral_constant<int, 1>{});
     act(std::integral_constant<int, 2>{});
     act(std::integral_constant<int, 3>{});
-    if (g.trace && tid == 0) g.trace[6 * blockIdx.x + 4] = rtime();  // (profiling) SiLU done
+    if (g.trace && !(g.dbg & 4096) && tid == 0) g.trace[6 * blockIdx.x + 4] = rtime();  // (profiling) SiLU done
     for (int half = 0; half < 2; ++half) {
-      if (half == 1 && g.trace && tid == 0) g.trace[6 * blockIdx.x + 5] = rtime();  // first half summed
+      if (half == 1 && g.trace && !(g.dbg & 4096) && tid == 0) g.trace[6 * blockIdx.x + 5] = rtime();  // first half summed
       if (wn == half) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -679,14 +685,21 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
           for (int u = 0; u < 8; ++u) sacc += v[u];
         }
         for (; j < ni.x; ++j) sacc += src[j * SEG_TP];
-        if (!(g.dbg & 4))
-          g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = sacc / (float)(ni.x < 1 ? 1 : ni.x);
+        const float mean = sacc / (float)(ni.x < 1 ? 1 : ni.x);
+        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = mean;
+        if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it (a wave = one node)
+          float m = fabsf(mean);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+          if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + seg.x + k, __float_as_uint(m));
+        }
       }
       __syncthreads();
     }
     if (g.trace && tid == 0) {
       unsigned long long* o = g.trace + 6 * blockIdx.x;
       o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
+      if (g.dbg & 4096) { o[4] = c0; o[5] = ctime(); }
     }
     return;
   }
@@ -699,6 +712,7 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
       if (tid == 0) {
         unsigned long long* o = g.trace + 6 * blockIdx.x;
         o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
+        if (g.dbg & 4096) { o[4] = c0; o[5] = ctime(); }
       }
     }
     return;
@@ -983,12 +997,13 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
   return hipGetLastError();
 }
 
-// W [N][K] -> split rows [N][K/32][hi 32 | lo 32] of W * 2^-e_n, e_n the exponent of
-// max_k |W[n][k]| (every scaled entry <= 1), and wscale[n] = 2^e_n. One block per row.
-// perm: store column 8q + 4h + e of each 32-chunk at 16h + 4q + e (the layout edge layer 1's
-// epilogue writes S in; applied to W2's K index).
+// W [N][K] -> split rows [N][K/cw][hi cw | lo cw] of W * 2^-e_n, e_n the exponent of
+// max_k |W[n][k]| (every scaled entry <= 1), and wscale[n] = 2^e_n. One block per row. cw = 32
+// for the edge GEMMs, 16 for the split16 node GEMMs.
+// perm (cw = 32): store column 8q + 4h + e of each 32-chunk at 16h + 4q + e (the layout edge
+// layer 1's epilogue writes S in; applied to W2's K index).
 __global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ W, int K, _Float16* __restrict__ out,
-                                                      float* __restrict__ wscale, int perm) {
+                                                      float* __restrict__ wscale, int perm, int cw) {
   __shared__ float red[4];
   const int n = blockIdx.x;
   const float* row = W + (long)n * K;
@@ -1005,16 +1020,17 @@ __global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ 
   for (int k = threadIdx.x; k < K; k += 256) {
     const float x = row[k] * sc;
     const _Float16 hi = (_Float16)x;
-    const int c = k % 32, pc = perm ? 16 * ((c >> 2) & 1) + 4 * (c >> 3) + (c & 3) : c;
-    o[(k / 32) * 64 + pc] = hi;
-    o[(k / 32) * 64 + 32 + pc] = (_Float16)(x - (float)hi);
+    const int c = k % cw, pc = perm ? 16 * ((c >> 2) & 1) + 4 * (c >> 3) + (c & 3) : c;
+    o[(k / cw) * 2 * cw + pc] = hi;
+    o[(k / cw) * 2 * cw + cw + pc] = (_Float16)(x - (float)hi);
   }
   if (threadIdx.x == 0) wscale[n] = ldexpf(1.0f, e);
 }
 
-hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s) {
-  if (K % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_split_rows_h, dim3(N), dim3(256), 0, s, W, K, reinterpret_cast<_Float16*>(out), wscale, perm);
+hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s, int chunk) {
+  if ((chunk != 32 && chunk != 16) || K % chunk || (perm && chunk != 32)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_split_rows_h, dim3(N), dim3(256), 0, s, W, K, reinterpret_cast<_Float16*>(out), wscale, perm,
+                     chunk);
   return hipGetLastError();
 }
 

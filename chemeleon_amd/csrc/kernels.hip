@@ -262,18 +262,28 @@ hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int*
 // ---------------------------------------------------------------------------
 // small node / graph kernels
 // ---------------------------------------------------------------------------
-__global__ void k_embed(const int64_t* __restrict__ a, const float* __restrict__ emb, float* __restrict__ Hout, long N,
-                        int P) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= N * P * (H / 4)) return;
-  const long r = idx / (H / 4);
-  const int q = (int)(idx - r * (H / 4));
-  const long i = r % N;
-  reinterpret_cast<f32x4*>(Hout + r * H)[q] = reinterpret_cast<const f32x4*>(emb + a[i] * H)[q];
+// one wave per row (4 rows per block); rmax != null: the row's max |value| for the split16 node GEMMs
+__global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, const float* __restrict__ emb,
+                                               float* __restrict__ Hout, long N, int P, float* __restrict__ rmax) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N * P) return;
+  const f32x4* e4 = reinterpret_cast<const f32x4*>(emb + a[r % N] * H);
+  const f32x4 v0 = e4[lane], v1 = e4[64 + lane];
+  f32x4* h4 = reinterpret_cast<f32x4*>(Hout + r * H);
+  h4[lane] = v0;
+  h4[64 + lane] = v1;
+  if (rmax) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(v0[k]), fabsf(v1[k])));
+    m = wave_max(m);
+    if (lane == 0) rmax[r] = m;
+  }
 }
-hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s) {
-  const long n = N * P * (H / 4);
-  hipLaunchKernelGGL(k_embed, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, emb, Hout, N, P);
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax) {
+  const long rows = N * P;
+  hipLaunchKernelGGL(k_embed, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, emb, Hout, N, P, rmax);
   return hipGetLastError();
 }
 
@@ -346,7 +356,8 @@ __device__ __forceinline__ void ln512(f32x4& v0, f32x4& v1, const float* w, cons
 __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, float* __restrict__ Hres,
                                                  float* __restrict__ Hl, const float* __restrict__ cond_emb,
                                                  const int* __restrict__ n2g, long N, int B, int P,
-                                                 const float* fw, const float* fb, const float* lw, const float* lb) {
+                                                 const float* fw, const float* fb, const float* lw, const float* lb,
+                                                 float* __restrict__ rmx, long rstride) {
   const int lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N * P) return;
@@ -370,12 +381,25 @@ __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, fl
   f32x4* l4 = reinterpret_cast<f32x4*>(Hl + r * H);
   l4[lane] = v0;
   l4[64 + lane] = v1;
+  if (rmx) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(v0[k]), fabsf(v1[k])));
+    m = wave_max(m);
+    if (lane == 0) {
+      rmx[RMX_HL * rstride + r] = m;
+      rmx[RMX_H * rstride + r] = 0.f;
+      rmx[RMX_AGG * rstride + r] = 0.f;
+      rmx[RMX_U * rstride + r] = 0.f;
+    }
+  }
 }
 hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
-                   const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s) {
+                   const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s, float* rmx,
+                   long rstride) {
   const long rows = N * P;
   hipLaunchKernelGGL(k_film_ln, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, Y, Hres, Hl, cond_emb, n2g, N, B,
-                     P, fw, fb, lw, lb);
+                     P, fw, fb, lw, lb, rmx, rstride);
   return hipGetLastError();
 }
 

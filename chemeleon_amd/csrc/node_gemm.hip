@@ -9,6 +9,15 @@
 // so the next K-tile's fragment reads and split run between the current tile's MFMAs.
 // Bit-identical to k_gemm3 (same products, same order); 5-10% faster in isolation.
 //
+// S16 (split16 mode): W pre-split into fp16 hi/lo rows [N][K/16][hi 16 | lo 16] of W * 2^-e_n
+// (split_rows_h, per-row power-of-two scale wscale[n] = 2^e_n, undone in the epilogue), A split by
+// each wave into fp16 hi/lo (round to nearest), three fp16 MFMA products (a_lo w_hi + a_hi w_lo +
+// a_hi w_hi): half the MFMAs of bf16x3, ~3.5 VALU per A element. A row r is scaled by 2^-e_r
+// before its split, e_r the exponent of max |A[r, :]| (g.amax / g.amax2, written by the kernel
+// that produced A: embed, film_ln, the segment-mean epilogue, or this kernel's own epilogue via
+// g.cmax), so every scaled entry is below 1 whatever the activations' range (the lattice terms
+// grow ~10^4x over a 1000-step trajectory); 2^e_r is applied again in the epilogue.
+//
 // 128x128 tiles, 256 threads (4 waves of 64x64, C^T accumulators as in gemm_bf16x3.hip),
 // K-tiles of 16, a 4-deep ring of 20 KB stages (3 K-tiles in flight), two blocks per CU.
 // LDS image per stage: A [128 rows][4 pieces of 4 fp32], piece p of row r at p ^ ((r >> 2) & 3);
@@ -32,9 +41,14 @@ constexpr int NM = 128, NN = 128, NK = 16;
 constexpr int A_ROWB = NK * 4, W_ROWB = NK * 2;  // 64 B, 32 B
 constexpr int A_STB = NM * A_ROWB;               // 8 KB
 constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
-constexpr int STB = A_STB + 3 * W_PLB;           // 20 KB
-constexpr int NST = 4;
-constexpr int NODE_LDS = NST * STB;              // 80 KB: two blocks per CU
+// bf16x3: A + three W planes (20 KB) x 4 stages; S16: A + W hi/lo rows (8 + 8 KB) x 5 stages
+template <bool S16> constexpr int STB = S16 ? A_STB + 2 * W_PLB : A_STB + 3 * W_PLB;
+template <bool S16> constexpr int NST = S16 ? 5 : 4;
+constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
+static_assert(STB<true> * NST<true> <= NODE_LDS && STB<false> * NST<false> <= NODE_LDS, "LDS");
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float silu_n(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
@@ -50,8 +64,9 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 }  // namespace
 
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR>
+template <int VAR, bool S16>
 __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
+  constexpr int STB_ = STB<S16>, NST_ = NST<S16>, AHEAD = NST_ - 1;  // K-tiles in flight
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -77,28 +92,39 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
     asrc[u] = g.A + ar * g.lda + 4 * alp;
     asrc2[u] = g.A2 + ar * g.lda2 + 4 * alp - g.ksplit;
   }
+  // W (bf16x3): instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1
+  // holding logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
+  // W (S16): rows of 64 B [hi 16 | lo 16] per K-tile, swizzled like A; instruction q (of 8) covers
+  // rows 16q + (L >> 2), LDS piece L & 3 holding logical piece alp; wave w issues q = 2w, 2w + 1.
+  constexpr int NWI = S16 ? 2 : 3;
   const int wlp = (lane & 1) ^ ((lane >> 4) & 1);
   const __bf16* Wpl = reinterpret_cast<const __bf16*>(g.Wp3);
   const long wplane = (long)g.N * g.K;
-  const __bf16* wsrc[3];
-  int wdst[3];
+  const __bf16* wsrc[NWI];
+  int wdst[NWI];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int q = 3 * wave + u, p = q >> 2, rq = q & 3;
-    wsrc[u] = Wpl + p * wplane + (long)(n0 + 32 * rq + (lane >> 1)) * g.K + 8 * wlp;
-    wdst[u] = A_STB + p * W_PLB + 32 * rq * W_ROWB;
+  for (int u = 0; u < NWI; ++u) {
+    if constexpr (S16) {
+      const int q = 2 * wave + u;
+      wsrc[u] = Wpl + (long)(n0 + 16 * q + (lane >> 2)) * 2 * g.K + 8 * alp;
+      wdst[u] = A_STB + q * 1024;
+    } else {
+      const int q = 3 * wave + u, p = q >> 2, rq = q & 3;
+      wsrc[u] = Wpl + p * wplane + (long)(n0 + 32 * rq + (lane >> 1)) * g.K + 8 * wlp;
+      wdst[u] = A_STB + p * W_PLB + 32 * rq * W_ROWB;
+    }
   }
   auto issue = [&](int t) {
     const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
-    char* st = lds + (t % NST) * STB;
+    char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (2 * wave + u) * A_ROWB), 16, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + k0), (lds_void*)(st + wdst[u]), 16, 0, 0);
+    for (int u = 0; u < NWI; ++u)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + (S16 ? 2 * k0 : k0)), (lds_void*)(st + wdst[u]), 16, 0, 0);
   };
 
   f32x16 acc[2][2];
@@ -111,61 +137,101 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
 
   // fragment offsets: A row wm*64 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
   const int asw = (r32 >> 2) & 3, wsw = (r32 >> 3) & 1;
+  // S16: this lane's two A rows (wm*64 + 32i + r32) and their power-of-two scales
+  float asc[2] = {1.0f, 1.0f}, aun[2] = {1.0f, 1.0f};
+  if constexpr (S16) {
+    if (g.amax) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int lr = wm * 64 + 32 * i + r32;
+        const long ar = row0 + (lr < nrows ? lr : nrows - 1);
+        float m = g.amax[ar];
+        if (g.amax2) m = fmaxf(m, g.amax2[ar]);
+        int e = 0;
+        if (m > 0.f) frexpf(m, &e);
+        asc[i] = ldexpf(1.0f, -e);
+        aun[i] = ldexpf(1.0f, e);
+      }
+    }
+  }
   const int fa0 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
   const int fa1 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
   const int fw = A_STB + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
+  const int fw16[2] = {A_STB + (wn * 64 + r32) * 64 + 16 * (h ^ asw),         // hi piece h
+                       A_STB + (wn * 64 + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
 
   // Software pipeline (VAR 0): while the 24 MFMAs of K-tile t run, the fragments of tile t+1 are
   // read from LDS and its A part is split, both interleaved between the MFMAs (the split's VALU
   // issues in the MFMAs' shadow). Fragment sets alternate, so the loop is unrolled by two.
+  constexpr int NP = S16 ? 2 : 3;  // operand parts
+  typedef std::conditional_t<S16, f16x8, bf16x8> frag;
   f32x4 ra0[2], ra1[2];
-  bf16x8 fa[2][3][2], fwt[2][3][2];  // [set][plane][i / j]
+  frag fa[2][NP][2], fwt[2][NP][2];  // [set][part][i / j]
   auto read_raw = [&](int t, int set) {
-    const char* st = lds + (t % NST) * STB;
+    const char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       ra0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
       ra1[i] = *reinterpret_cast<const f32x4*>(st + fa1 + i * 32 * A_ROWB);
     }
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        fwt[set][p][j] = *reinterpret_cast<const bf16x8*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
+        fwt[set][p][j] = S16 ? *reinterpret_cast<const frag*>(st + fw16[p] + j * 32 * 64)
+                             : *reinterpret_cast<const frag*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
   };
   auto split = [&](int set) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (S16) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        __bf16 x0, x1, x2;
-        if (VAR == 1) {
-          x0 = x1 = x2 = (__bf16)(e < 4 ? ra0[i][e] : ra1[i][e - 4]);
-        } else {
-          split3n(e < 4 ? ra0[i][e] : ra1[i][e - 4], x0, x1, x2);
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 x = (e < 4 ? f32x2{ra0[i][e], ra0[i][e + 1]} : f32x2{ra1[i][e - 4], ra1[i][e - 3]}) * asc[i];
+          const f16x2 hi = __builtin_convertvector(x, f16x2);
+          const f16x2 lo = VAR == 1 ? hi : __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
+          fa[set][0][i][e] = hi[0]; fa[set][0][i][e + 1] = hi[1];
+          fa[set][1][i][e] = lo[0]; fa[set][1][i][e + 1] = lo[1];
         }
-        fa[set][0][i][e] = x0;
-        fa[set][1][i][e] = x1;
-        fa[set][2][i][e] = x2;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 x0, x1, x2;
+          if (VAR == 1) {
+            x0 = x1 = x2 = (__bf16)(e < 4 ? ra0[i][e] : ra1[i][e - 4]);
+          } else {
+            split3n(e < 4 ? ra0[i][e] : ra1[i][e - 4], x0, x1, x2);
+          }
+          fa[set][0][i][e] = x0;
+          fa[set][1][i][e] = x1;
+          fa[set][2][i][e] = x2;
+        }
       }
+    }
   };
   // small terms first, the leading product last (as gemm_bf16x3.hip)
-  constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
-  constexpr int PW[6] = {0, 1, 2, 0, 1, 0};
+  constexpr int PA[6] = {S16 ? 1 : 2, S16 ? 0 : 1, 0, 1, 0, 0};
+  constexpr int PW[6] = {0, 1, S16 ? 0 : 2, 0, 1, 0};
   auto mfmas = [&](int set, int k0, int k1) {
 #pragma unroll
     for (int k = k0; k < k1; ++k)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fwt[set][PW[k]][j], fa[set][PA[k]][i], acc[i][j], 0, 0,
-                                                               0);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (S16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fwt[set][PW[k]][j], fa[set][PA[k]][i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fwt[set][PW[k]][j], fa[set][PA[k]][i], acc[i][j], 0, 0,
+                                                                 0);
+        }
   };
-  issue(0);
-  issue(1);
-  issue(2);
-  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < AHEAD; ++t) issue(t);
+  if constexpr (S16)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // (AHEAD - 1) tiles x 4 loads
+  else
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // (AHEAD - 1) tiles x 5 loads
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read_raw(0, 0);
@@ -173,27 +239,48 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
   split(0);
   auto step = [&](int t, auto CUR) {
     constexpr int cur = decltype(CUR)::value;
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // this thread's part of tile t+1 has landed
+    // this thread's part of tile t+1 has landed (AHEAD - 2 tiles may stay in flight)
+    if constexpr (S16)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage has been read
     asm volatile("" ::: "memory");
-    issue(t + 3);                                     // past the end: re-reads into the free stage
+    issue(t + AHEAD);                                 // past the end: re-reads into the free stage
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
-    mfmas(cur, 0, 2);                                 // 8 MFMAs beside the 10 fragment reads
+    if constexpr (S16) {
+      mfmas(cur, 0, 1);                               // 4 MFMAs beside the 8 fragment reads
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    split(cur ^ 1);
-    mfmas(cur, 2, 6);                                 // 16 MFMAs, the split's VALU between them
+      for (int k = 0; k < 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      split(cur ^ 1);
+      mfmas(cur, 1, 3);                               // 8 MFMAs, the split's VALU between them
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+      }
+    } else {
+      mfmas(cur, 0, 2);                               // 8 MFMAs beside the 10 fragment reads
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      split(cur ^ 1);
+      mfmas(cur, 2, 6);                               // 16 MFMAs, the split's VALU between them
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
+      }
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -208,37 +295,50 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const long lr = wm * 64 + i * 32 + r32;
-    if (lr >= nrows) continue;
-    const long row = row0 + lr;
-    const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
+    float cm = 0.f;  // max |C| over this lane's columns of the row
+    if (lr < nrows) {
+      const long row = row0 + lr;
+      const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
-        f32x4 v;
+        for (int q = 0; q < 4; ++q) {
+          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
+          f32x4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-        if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
-        if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
-        if (g.act == 1)
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          if constexpr (S16) v *= *reinterpret_cast<const f32x4*>(g.wscale + col) * aun[i];  // undo the scales
+          if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+          if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+          if (g.act == 1)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
-        if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
-        *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+            for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
+          if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+          *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+          if constexpr (S16) cm = fmaxf(cm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+    }
+    if constexpr (S16) {
+      if (g.cmax) {  // lanes r32 and r32 + 32 hold the same row
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        if (h == 0 && lr < nrows) atomicMax(g.cmax + row0 + lr, __float_as_uint(cm));
       }
+    }
   }
 }
 
 int g_node_variant = 0;
 
 hipError_t node_gemm_init() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_node_gemm<0>, hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_node_gemm<1>, hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
+  const void* ks[4] = {(const void*)k_node_gemm<0, false>, (const void*)k_node_gemm<1, false>,
+                       (const void*)k_node_gemm<0, true>, (const void*)k_node_gemm<1, true>};
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
   return e;
 }
 
+// bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
+// rows of 16-column chunks, g.wscale = their row scales)
 hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
   if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
@@ -249,10 +349,11 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
     attr = true;
   }
   const long blocks = ((g.M + NM - 1) / NM) * (g.N / NN);
-  if (g_node_variant == 1)
-    hipLaunchKernelGGL(k_node_gemm<1>, dim3((unsigned)blocks), dim3(256), NODE_LDS, s, g);
+  const dim3 grid((unsigned)blocks), block(256);
+  if (g.wscale)
+    hipLaunchKernelGGL((g_node_variant == 1 ? k_node_gemm<1, true> : k_node_gemm<0, true>), grid, block, NODE_LDS, s, g);
   else
-    hipLaunchKernelGGL(k_node_gemm<0>, dim3((unsigned)blocks), dim3(256), NODE_LDS, s, g);
+    hipLaunchKernelGGL((g_node_variant == 1 ? k_node_gemm<1, false> : k_node_gemm<0, false>), grid, block, NODE_LDS, s, g);
   return hipGetLastError();
 }
 

@@ -37,6 +37,8 @@ struct LayerW {
   const void *WAB3, *D3, *W23, *W33, *W43;  // bf16 hi/mid/lo planes of the GEMM weights
   void *D2h, *W22h;                          // fp16 hi/lo planes of the edge-GEMM weights (row-scaled)
   float *Dsc, *W2sc;                         // their per-row power-of-two scales
+  void *WAB16, *W316, *W416;                 // split16 node GEMMs: fp16 hi/lo rows, 16-column chunks
+  float *WABsc, *W3sc, *W4sc;                // (row-scaled like D2h)
 };
 
 enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1, MATH_SPLIT16 = 2 };
@@ -50,9 +52,13 @@ struct chm_model {
   const void *Wc3, *Wp3, *Whead3;
   void* mem3 = nullptr;  // bf16 planes arena
   void* mem2 = nullptr;  // fp16 planes + scales arena
+  void* mem16 = nullptr; // split16 node-GEMM weights arena
+  const void* Wp16 = nullptr;
+  float* Wpsc = nullptr;
   int math = MATH_SPLIT16;
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
+  int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
   int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
@@ -74,6 +80,7 @@ struct chm_batch {
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
+  float* rmx;        // split16 node GEMMs: the four row-max arrays [4][P*N] (RMX_*)
   unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
   std::vector<void*> allocs;
   size_t bytes = 0;
@@ -217,6 +224,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->edge_dbg = dbg ? atoi(dbg) : 0;
     const char* ng = getenv("CHM_NODE_GLDS");
     if (ng) m->node_glds = atoi(ng);
+    const char* n16 = getenv("CHM_NODE16");
+    if (n16) m->node16 = atoi(n16);
     const char* pp = getenv("CHM_EDGE1_PP");
     if (pp) m->edge1_pp = atoi(pp);
     m->edge_trace = getenv("CHM_EDGE_TRACE");
@@ -268,9 +277,34 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, 0, s);
       if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, 1, s);  // K permuted like S
     }
+    // fp16 hi/lo rows (16-column chunks, + row scales) of the node-GEMM weights (split16 node GEMMs)
+    if (e2 == hipSuccess) {
+      struct J16 { const float* src; int n, k; void** dst; float** sc; };
+      std::vector<J16> j16;
+      void* wp16 = nullptr;
+      j16.push_back({m->Wp, H, H, &wp16, &m->Wpsc});
+      for (auto& w : m->layers) {
+        j16.push_back({w.WAB, 2 * H, H, &w.WAB16, &w.WABsc});
+        j16.push_back({w.W3, H, 2 * H, &w.W316, &w.W3sc});
+        j16.push_back({w.W4, H, H, &w.W416, &w.W4sc});
+      }
+      auto sz = [](const J16& j) { return ((size_t)j.n * j.k * 4 + 255) / 256 * 256 + ((size_t)j.n * 4 + 255) / 256 * 256; };
+      size_t tot = 0;
+      for (auto& j : j16) tot += sz(j);
+      e2 = hipMalloc(&m->mem16, tot);
+      char* q = (char*)m->mem16;
+      for (auto& j : j16) {
+        if (e2 != hipSuccess) break;
+        *j.dst = q;
+        *j.sc = (float*)(q + ((size_t)j.n * j.k * 4 + 255) / 256 * 256);
+        e2 = split_rows_h(j.src, j.n, j.k, *j.dst, *j.sc, 0, s, 16);
+        q += sz(j);
+      }
+      m->Wp16 = wp16;
+    }
     if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
     if (e2 != hipSuccess) {
-      (void)hipFree(m->mem); (void)hipFree(m->mem3); (void)hipFree(m->mem2);
+      (void)hipFree(m->mem); (void)hipFree(m->mem3); (void)hipFree(m->mem2); (void)hipFree(m->mem16);
       delete m;
       return fail(CHM_E_HIP, std::string("plane split: ") + hipGetErrorString(e2));
     }
@@ -294,6 +328,7 @@ extern "C" void chm_model_destroy(chm_model* m) {
   (void)hipFree(m->mem);
   (void)hipFree(m->mem3);
   (void)hipFree(m->mem2);
+  (void)hipFree(m->mem16);
   delete m;
 }
 
@@ -391,6 +426,7 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->S = fl(((size_t)P * E + kTileRows) * H);
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
+  b->rmx = fl((size_t)4 * P * N);
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
   b->LAT = fl((size_t)P * B * 9);
@@ -495,8 +531,14 @@ static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const floa
   return g;
 }
 
-static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s) {
+// W16 / wsc: the split16 node-GEMM rows of the same weight (null: bf16x3 in every mode)
+static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s,
+                           const void* W16 = nullptr, const float* wsc = nullptr) {
   if (b->math == MATH_F32) return gemm(g, epi, s);
+  if (b->math == MATH_SPLIT16 && W16 && g.amax && b->m->node16 && b->m->node_glds && epi == EPI_STD) {
+    g.Wp3 = W16; g.wscale = wsc;
+    return node_gemm(g, s);
+  }
   g.Wp3 = W3;
   if (epi == EPI_STD && b->m->node_glds) return node_gemm(g, s);
   return gemm_bf16x3(g, epi, s);
@@ -536,7 +578,7 @@ static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which
       fclose(f);
     }
   }
-  hipFree(tbuf);
+  (void)hipFree(tbuf);
   return e;
 }
 
@@ -549,13 +591,17 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   const long N = b->N, E = b->E, R = (long)P * N;
   const int CIN = TD + X;
   ProfScope whole(CHM_K_DECODER, s);
+  // split16 node GEMMs: row maxima of their A operands, written by the producing kernels
+  const bool n16 = b->math == MATH_SPLIT16 && m->node16 && m->node_glds;
+  const long RS = (long)b->P * N;
+  auto rmx = [&](int k) { return n16 ? b->rmx + k * RS : nullptr; };
   HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
   {
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
-  HIPCHK(embed(a, m->emb, b->Hres, N, P, s));
+  HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H)));
   if (b->math == MATH_SPLIT16)
     HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s));  // fp16 hi/lo planes [2][E][768] in F's bytes
   else
@@ -566,14 +612,15 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     const LayerW& w = m->layers[l];
     {  // FiLM projection (cspnet.py:92)
       GemmArgs g = gargs(R, H, H, b->Hres, H, m->Wp, b->Y, H);
-      g.bias = m->bp;
-      HIPCHK(run_gemm(b, g, EPI_STD, m->Wp3, s));
+      g.bias = m->bp; g.amax = rmx(RMX_H);
+      HIPCHK(run_gemm(b, g, EPI_STD, m->Wp3, s, m->Wp16, m->Wpsc));
     }
-    HIPCHK(film_ln(b->Y, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s));
+    HIPCHK(film_ln(b->Y, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s, rmx(0), RS));
     {  // per-node halves of the first edge layer: [P | Q] = Hl [A ; Bm]^T, P += b1 + C vec(LL^T)
       GemmArgs g = gargs(R, 2 * H, H, b->Hl, H, w.WAB, b->PQ, 2 * H);
       g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
-      HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s));
+      g.amax = rmx(RMX_HL);
+      HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s, w.WAB16, w.WABsc));
     }
     if (b->math == MATH_SPLIT16) {
       // split16: fp16 hi/lo split rows throughout (edge_gemm.hip). S lives in S's bytes as
@@ -597,7 +644,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
         ea.W = w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles; ea.ntiles = b->ntiles;
         ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
-        ea.node_n = b->node_n;
+        ea.node_n = b->node_n; ea.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
         ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
         HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] { return edge_gemm(ea, EPI_SEGMEAN, s); }));
@@ -629,19 +676,21 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     {  // node MLP 1: U = SiLU([Hl | agg] W3^T + b3)
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);
       g.A2 = b->agg; g.lda2 = H; g.ksplit = H; g.bias = w.b3; g.act = 1;
-      HIPCHK(run_gemm(b, g, EPI_STD, w.W33, s));
+      g.amax = rmx(RMX_HL); g.amax2 = rmx(RMX_AGG); g.cmax = reinterpret_cast<unsigned*>(rmx(RMX_U));
+      HIPCHK(run_gemm(b, g, EPI_STD, w.W33, s, w.W316, w.W3sc));
     }
     {  // node MLP 2 + residual: Hres += SiLU(U W4^T + b4)
       GemmArgs g = gargs(R, H, H, b->Y, H, w.W4, b->Hres, H);
       g.bias = w.b4; g.act = 1; g.R = b->Hres; g.ldr = H;
-      HIPCHK(run_gemm(b, g, EPI_STD, w.W43, s));
+      g.amax = rmx(RMX_U); g.cmax = reinterpret_cast<unsigned*>(rmx(RMX_H));
+      HIPCHK(run_gemm(b, g, EPI_STD, w.W43, s, w.W416, w.W4sc));
     }
   }
   HIPCHK(layer_norm(b->Hres, b->Hf, R, m->flw, m->flb, s));
   if (heads & 1) {
     GemmArgs g = gargs(R, HEADS_N, H, b->Hf, H, m->Whead, b->HO, HEADS_N);
     g.bias = m->bhead;
-    HIPCHK(run_gemm(b, g, EPI_STD, m->Whead3, s));
+    HIPCHK(run_gemm(b, g, EPI_STD, m->Whead3, s));  // (bf16x3: A is LayerNorm output, M small)
   }
   if (heads & 2) HIPCHK(graph_heads(b->Hf, m->Wlat, lat, b->node_off, b->natoms, N, B, P, b->LAT, s));
   return CHM_OK;

@@ -3,6 +3,7 @@
 //         chemeleon_amd/csrc/gemm_bf16x3.hip -o tools/gemm_bench && tools/gemm_bench
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -153,14 +154,39 @@ int main(int argc, char** argv) {
       printf("M=%ld N=%d K=%d  k_gemm3 %.1f us %.1f TF | k_node_gemm %.1f us %.1f TF (no bias/act %.1f us, no split %.1f us)\n",
              M, N, K, tr * 1e3, flops / tr / 1e9, tn * 1e3, flops / tn / 1e9, tn0 * 1e3, tv * 1e3);
     }
-    std::vector<float> c1(65536), c2(65536);
+    // split16 variant: W as 16-column fp16 hi/lo rows with row scales
+    void* W16; float* wsc16;
+    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4));
+    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
+    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16;
+    for (int rep = 0; rep < 2; ++rep) {
+      float t16 = time_it(10, s, [&] { CK(node_gemm(g16, s)); });
+      GemmArgs g160 = g16; g160.bias = nullptr; g160.act = 0;
+      float t160 = time_it(10, s, [&] { CK(node_gemm(g160, s)); });
+      g_node_variant = 1;
+      float t16v = time_it(10, s, [&] { CK(node_gemm(g160, s)); });
+      g_node_variant = 0;
+      printf("  split16 k_node_gemm %.1f us %.1f TF (no bias/act %.1f us, no split %.1f us)\n", t16 * 1e3,
+             flops / t16 / 1e9, t160 * 1e3, t16v * 1e3);
+    }
+    const size_t nc = (size_t)std::min<long>(M, 4096) * N;
+    std::vector<float> c1(nc), c2(nc), c3(nc);
+    CK(gemm(g, EPI_STD, s)); CK(hipStreamSynchronize(s));  // fp32 MFMA reference
+    CK(hipMemcpy(c3.data(), C, nc * 4, hipMemcpyDeviceToHost));
     CK(gemm_bf16x3(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(c1.data(), C, nc * 4, hipMemcpyDeviceToHost));
     CK(node_gemm(g, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
-    double mx = 0;
-    for (size_t i = 0; i < c1.size(); ++i) mx = fmax(mx, fabs((double)c1[i] - c2[i]));
-    printf("  max |node - gemm3| = %.3e\n", mx);
+    CK(hipMemcpy(c2.data(), C, nc * 4, hipMemcpyDeviceToHost));
+    double mx = 0, e3 = 0, e16 = 0, ref = 0;
+    for (size_t i = 0; i < nc; ++i) {
+      mx = fmax(mx, fabs((double)c1[i] - c2[i]));
+      e3 = fmax(e3, fabs((double)c1[i] - c3[i]));
+      ref = fmax(ref, fabs((double)c3[i]));
+    }
+    CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c2.data(), C, nc * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nc; ++i) e16 = fmax(e16, fabs((double)c2[i] - c3[i]));
+    printf("  max |node - gemm3| = %.3e; vs f32 MFMA: bf16x3 %.3e, split16 %.3e (max |C| %.3e)\n", mx, e3, e16, ref);
     return 0;
   }
   float t32 = time_it(5, s, [&] { CK(gemm(g, EPI_STD, s)); });

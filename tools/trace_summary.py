@@ -14,7 +14,11 @@ print(f"blocks {len(a)}  span {te.max() / 100:.1f} us  CUs {len(np.unique(hw))}"
 main, epi = (tm - t0) / 100, (te - tm) / 100
 t4, t5 = a[:, 4].astype(np.int64) - base, a[:, 5].astype(np.int64) - base
 ok = a[:, 4] > 0
-if ok.any():
+if ok.any() and "--clock" in sys.argv:  # CHM_EDGE_DBG=4096: slots 4, 5 = s_memtime at block start / end
+    f = (a[:, 5].astype(np.int64) - a[:, 4].astype(np.int64))[ok] / ((te - t0)[ok] / 100)
+    print(f"shader clock over each block: median {np.median(f):.0f} MHz (p10 {np.percentile(f, 10):.0f}, "
+          f"p90 {np.percentile(f, 90):.0f})")
+elif ok.any():
     print(f"epilogue split (markers 4, 5): tm->4 {np.median((t4 - tm)[ok]) / 100:.1f} us, "
           f"4->5 {np.median((t5 - t4)[ok]) / 100:.1f} us, 5->end {np.median((te - t5)[ok]) / 100:.1f} us "
           f"({ok.sum()} blocks)")
