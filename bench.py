@@ -269,7 +269,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": {"f32": "f32", "bf16x3": "f32 (bf16x3-split MFMA, fp32 accumulate)",
-                  "split16": "f32 (fp16x2-split edge GEMMs / bf16x3 node GEMMs, fp32 accumulate)"}[math],
+                  "split16": "f32 (fp16x2-split edge and node GEMMs with power-of-two row scales, fp32 accumulate)"}[math],
         "data": "synthetic (seeded random-init weights of the real architecture; seeded conditioning vectors)",
         "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
