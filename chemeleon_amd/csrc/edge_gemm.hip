@@ -59,6 +59,18 @@ constexpr int PRE_ROW1 = 63, PRE_MAX = 61;
 __device__ __forceinline__ float silu_e(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
+// the same on a pair, written with 2-wide vectors so the multiplies and adds issue packed
+// (v_pk_mul_f32 / v_pk_add_f32: half the VALU slots; bit-identical to silu_e per element)
+typedef float f32x2e __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2e silu_e2(f32x2e x) {
+  f32x2e t = x * -1.44269504088896341f;
+  t.x = __builtin_amdgcn_exp2f(t.x);
+  t.y = __builtin_amdgcn_exp2f(t.y);
+  t = t + 1.0f;
+  t.x = __builtin_amdgcn_rcpf(t.x);
+  t.y = __builtin_amdgcn_rcpf(t.y);
+  return x * t;
+}
 
 __device__ __forceinline__ long remap(long b, long nb) {
   const long q = nb / 8, r = nb % 8, xcd = b % 8, idx = b / 8;
@@ -179,11 +191,17 @@ __device__ __forceinline__ void edge_epilogue(const EdgeArgs& g, f32x16 (&acc)[2
             const f32x4 p = *reinterpret_cast<const f32x4*>(prow + j * 32 + 8 * q);
             const f32x4 qv = *reinterpret_cast<const f32x4*>(qrow + j * 32 + 8 * q);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x = silu_e((acc[i][j][4 * q + e] + p[e]) + qv[e]);
-              mx = fmaxf(mx, fabsf(x));
-              if constexpr (last) acc[i][j][4 * q + e] = x;
-              else v[j][q][e] = x;
+            for (int e = 0; e < 4; e += 2) {
+              const f32x2e a2 = {acc[i][j][4 * q + e], acc[i][j][4 * q + e + 1]};
+              const f32x2e x = silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{qv[e], qv[e + 1]});
+              mx = fmaxf(mx, fmaxf(fabsf(x.x), fabsf(x.y)));
+              if constexpr (last) {
+                acc[i][j][4 * q + e] = x.x;
+                acc[i][j][4 * q + e + 1] = x.y;
+              } else {
+                v[j][q][e] = x.x;
+                v[j][q][e + 1] = x.y;
+              }
             }
           }
         auto val = [&](int j, int q, int e) {
@@ -634,8 +652,13 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc[i][j][4 * q + e] = silu_e(acc[i][j][4 * q + e] * (sc[j & 1][q][e] * rs[i]) + bb[j & 1][q][e]);
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2e a2 = {acc[i][j][4 * q + e], acc[i][j][4 * q + e + 1]};
+            const f32x2e s2 = f32x2e{sc[j & 1][q][e], sc[j & 1][q][e + 1]} * rs[i];
+            const f32x2e x = silu_e2(a2 * s2 + f32x2e{bb[j & 1][q][e], bb[j & 1][q][e + 1]});
+            acc[i][j][4 * q + e] = x.x;
+            acc[i][j][4 * q + e + 1] = x.y;
+          }
       // pin this group's math ahead of the next group's loads (which stay behind the clobber)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
