@@ -18,9 +18,15 @@ Noise
   kernels from a counter-based Philox stream keyed by (seed, t, global
   node / graph index); results do not depend on how samples are sharded.
 
-Text conditioning is out of scope for the hot path (north star: "computed
-once on host and broadcast"): pass a `text_encoder` object with the
-reference's `get_text_embeds(texts, cond_drop_prob, device)` method, or pass
+Text conditioning runs once per call on the host side of the boundary (north
+star: "computed once on host and broadcast"). As in the reference
+(chemeleon.py:37-52), a text_guide model builds its
+`chemeleon_amd.text_encoder.TextEncoder` from the config (`text_encoder`,
+`text_embed_dim`, `max_text_len`, `text_dim`, optional `path_ckpt_clip=`
+CrystalCLIP checkpoint) — here only when a local copy of the language model is
+available (`text_model_dir=` or $CHEMELEON_TEXT_MODEL_DIR; nothing is
+downloaded). Alternatively pass any `text_encoder` object with the reference's
+`get_text_embeds(texts, cond_drop_prob, device)` method, or pass
 `text_embeds=` / `null_text_embeds=` tensors directly.
 """
 
@@ -52,6 +58,8 @@ class Chemeleon(nn.Module):
         self.time_embed = SinusoidalTimeEmbeddings(cfg["time_dim"])
         self.text_guide = cfg["text_guide"]
         self.cond_drop_prob = cfg.get("cond_drop_prob", 0.2)
+        if text_encoder is None and self.text_guide:
+            text_encoder = self._build_text_encoder(cfg, kwargs)
         self.text_encoder = text_encoder
         self.num_timesteps = cfg["timesteps"]
         self.beta_scheduler = BetaScheduler(timesteps=self.num_timesteps, scheduler_mode=cfg["beta_schedule"])
@@ -68,6 +76,22 @@ class Chemeleon(nn.Module):
                               pred_atom_types=cfg["pred_atom_types"])
         self._tables: Dict[Tuple, Tuple] = {}
 
+    @staticmethod
+    def _build_text_encoder(cfg, kwargs):
+        """reference chemeleon.py:37-52, from local files only; None when no
+        local language model is configured (then texts need an injected encoder)."""
+        tdir = kwargs.get("text_model_dir")
+        if tdir is None and not os.environ.get("CHEMELEON_TEXT_MODEL_DIR"):
+            return None
+        from chemeleon_amd.text_encoder import CrystalClip, TextEncoder
+        clip = None
+        if kwargs.get("path_ckpt_clip"):
+            clip = CrystalClip.load_from_checkpoint(kwargs["path_ckpt_clip"], text_model_dir=tdir)
+        return TextEncoder(text_encoder_name=cfg["text_encoder"], text_embed_dim=cfg["text_embed_dim"],
+                           max_text_len=cfg["max_text_len"], text_dim=cfg["text_dim"],
+                           trainable_text_encoder=cfg["trainable_text_encoder"], pretrained_clip_model=clip,
+                           local_path=None if clip is not None else tdir)
+
     # ------------------------------------------------------------------ loading
     @property
     def device(self):
@@ -80,17 +104,19 @@ class Chemeleon(nn.Module):
         Buffers (schedules, sigmas_norm, D3PM tables) come from the file."""
         ck = torch.load(path, map_location=map_location, weights_only=True)
         hp = dict(ck.get("hyper_parameters", {}))
+        extra = {k: kwargs.pop(k) for k in ("text_model_dir", "path_ckpt_clip") if k in kwargs}
         hp.update(kwargs)
-        m = cls(hp, text_encoder=text_encoder)
+        m = cls(hp, text_encoder=text_encoder, **extra)
         sd = ck["state_dict"]
         own = {k: v for k, v in sd.items() if not k.startswith("text_encoder.")}
         missing, unexpected = m.load_state_dict(own, strict=False)
+        missing = [k for k in missing if not k.startswith("text_encoder.")]
         if strict and (missing or unexpected):
             raise RuntimeError(f"checkpoint mismatch: missing {missing}, unexpected {unexpected}")
-        if text_encoder is not None and isinstance(text_encoder, nn.Module):
+        if m.text_encoder is not None and isinstance(m.text_encoder, nn.Module):
             te = {k[len("text_encoder."):]: v for k, v in sd.items() if k.startswith("text_encoder.")}
             if te:
-                text_encoder.load_state_dict(te, strict=False)
+                m.text_encoder.load_state_dict(te, strict=False)
         return m
 
     @classmethod

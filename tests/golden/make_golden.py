@@ -396,6 +396,74 @@ def gen_state_keys(chm, csp):
     print("wrote", path, len(keys), "keys")
 
 
+TINY_BERT_WORDS = ("[PAD] [UNK] [CLS] [SEP] [MASK] a an of the with and in crystal cubic hexagonal structure oxide "
+                   "ti o 2 3 4 li fe p mn si n ba sr group space").split()
+
+
+def build_tiny_bert(real_tf, out_dir):
+    """A 2-layer, 32-wide BERT with a 36-word vocabulary, seeded, saved to `out_dir` (the
+    test reloads it from there: no network and no pretrained weights anywhere)."""
+    os.makedirs(out_dir, exist_ok=True)
+    vocab = os.path.join(out_dir, "vocab.txt")
+    with open(vocab, "w") as f:
+        f.write("\n".join(TINY_BERT_WORDS) + "\n")
+    tok = real_tf.BertTokenizer(vocab)
+    torch.manual_seed(1234)
+    cfg = real_tf.BertConfig(vocab_size=len(TINY_BERT_WORDS), hidden_size=32, num_hidden_layers=2,
+                             num_attention_heads=4, intermediate_size=64, max_position_embeddings=32)
+    bert = real_tf.BertModel(cfg).eval()
+    bert.save_pretrained(out_dir)
+    tok.save_pretrained(out_dir)
+    return bert, tok
+
+
+def gen_text(chm, csp):
+    """Conditioning front-end: the reference TextEncoder
+    (chemeleon/text_encoder/text_encoder.py:22-205) on a tiny seeded local BERT, through its
+    CrystalCLIP branch (`pretrained_clip_model`, whose `text_proj` is applied) and with that
+    branch detached (plain [CLS] embedding). The reference's `_setup_text_encoder` would fetch
+    the model from the hub, so the encoder and tokenizer are handed in through a stand-in CLIP
+    object. transformers 5.x dropped `batch_encode_plus`, which the reference calls; the
+    tokenizer is wrapped so that name forwards to `__call__` (what it was in 4.x for a list)."""
+    import chemeleon.text_encoder.text_encoder as rte  # (bound to the class stubs; unused below)
+    sys.modules.pop("transformers")  # the real package from here on (lazy submodule imports)
+    sys.modules.pop("wandb")  # (transformers probes optional packages with find_spec)
+    import transformers as real_tf
+
+    out_dir = os.path.join(HERE, "tiny_bert")
+    bert, tok = build_tiny_bert(real_tf, out_dir)
+
+    class Tok:
+        def __init__(self, t):
+            self.t = t
+
+        def batch_encode_plus(self, texts, **kw):
+            return self.t(texts, **kw)
+
+    torch.manual_seed(99)
+    clip = nn.Module()
+    clip.text_encoder, clip.tokenizer = bert, Tok(tok)
+    clip.text_proj = nn.Sequential(nn.Linear(32, 32), nn.LayerNorm(32), nn.GELU(), nn.Linear(32, 32))
+    te = rte.TextEncoder(text_encoder_name="lfoppiano/MatTPUSciBERT", text_embed_dim=32, max_text_len=12,
+                         text_dim=24, pretrained_clip_model=clip)
+    texts = ["Ti O2", "a cubic crystal structure of Li Fe P O4 with space group",
+             "hexagonal Ba Ti O3", "Mn O", "a crystal of Sr Ti O3 and the oxide of Si O2 in a cubic structure"]
+    out = {}
+    with torch.no_grad():
+        out["clip_cond"] = te.get_text_embeds(texts, cond_drop_prob=0.0, device="cpu")
+        out["clip_null"] = te.get_text_embeds(texts, cond_drop_prob=1.0, device="cpu")
+        torch.manual_seed(5)
+        out["clip_drop05"] = te.get_text_embeds(texts, cond_drop_prob=0.5, device="cpu")
+        out["clip_encode"] = te.text_encode(texts, device="cpu")
+        te.clip_model = None  # the plain-BERT branch: [CLS] row, no projection
+        out["bert_encode"] = te.text_encode(texts, device="cpu")
+        out["bert_cond"] = te.get_text_embeds(texts, cond_drop_prob=0.0, device="cpu")
+    sd = {k: v for k, v in te.state_dict().items() if not k.startswith("text_encoder.")}
+    arrs = {f"w:{k}": v for k, v in sd.items()}
+    arrs.update({f"p:{k}": v for k, v in clip.text_proj.state_dict().items()})
+    save("text_encoder.npz", texts=np.array(texts), **out, **arrs)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(os.path.join(REF, "chemeleon")):
         print("reference not present; nothing to do")
@@ -415,5 +483,7 @@ if __name__ == "__main__":
         gen_trajectory(chm, csp)
     if "keys" in which:
         gen_state_keys(chm, csp)
+    if "text" in which:
+        gen_text(chm, csp)
     if "trajectory1000" in which:
         gen_trajectory(chm, csp, T=1000, every=10)
