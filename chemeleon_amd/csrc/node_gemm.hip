@@ -19,7 +19,8 @@
 // grow ~10^4x over a 1000-step trajectory); 2^e_r is applied again in the epilogue.
 //
 // 128x128 tiles, 256 threads (4 waves of 64x64, C^T accumulators as in gemm_bf16x3.hip),
-// K-tiles of 16, a 4-deep ring of 20 KB stages (3 K-tiles in flight), two blocks per CU.
+// K-tiles of 16, a 4-deep ring of 20 KB stages (3 K-tiles in flight), two blocks per CU; S16 uses
+// 16 KB stages, 5 deep with two blocks per CU or 3 deep with three (large grids).
 // LDS image per stage: A [128 rows][4 pieces of 4 fp32], piece p of row r at p ^ ((r >> 2) & 3);
 // W plane q [128 rows][2 pieces of 8 bf16], piece p of row r at p ^ ((r >> 3) & 1): the
 // fragment reads of every 16-lane group then cover all 64 banks.
@@ -43,9 +44,12 @@ constexpr int A_STB = NM * A_ROWB;               // 8 KB
 constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
 // bf16x3: A + three W planes (20 KB) x 4 stages; S16: A + W hi/lo rows (8 + 8 KB) x 5 stages
 template <bool S16> constexpr int STB = S16 ? A_STB + 2 * W_PLB : A_STB + 3 * W_PLB;
-template <bool S16> constexpr int NST = S16 ? 5 : 4;
+// NB = blocks per CU: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of 16 KB)
+template <bool S16, int NB> constexpr int NST = NB == 3 ? 3 : (S16 ? 5 : 4);
 constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
-static_assert(STB<true> * NST<true> <= NODE_LDS && STB<false> * NST<false> <= NODE_LDS, "LDS");
+static_assert(STB<true> * NST<true, 2> <= NODE_LDS && STB<false> * NST<false, 2> <= NODE_LDS, "LDS");
+static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -64,9 +68,11 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 }  // namespace
 
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR, bool S16>
-__global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
-  constexpr int STB_ = STB<S16>, NST_ = NST<S16>, AHEAD = NST_ - 1;  // K-tiles in flight
+template <int VAR, bool S16, int NB>
+__global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
+  static_assert(NB == 2 || (S16 && NB == 3), "blocks per CU");
+  constexpr int STB_ = STB<S16>, NST_ = NST<S16, NB>, AHEAD = NST_ - 1;  // K-tiles in flight
+  constexpr int GL = S16 ? 4 : 5;                                        // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -228,10 +234,7 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
   };
 #pragma unroll
   for (int t = 0; t < AHEAD; ++t) issue(t);
-  if constexpr (S16)
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // (AHEAD - 1) tiles x 4 loads
-  else
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // (AHEAD - 1) tiles x 5 loads
+  vm_wait<(AHEAD - 1) * GL>();  // tile 0 has landed
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read_raw(0, 0);
@@ -240,10 +243,7 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
   auto step = [&](int t, auto CUR) {
     constexpr int cur = decltype(CUR)::value;
     // this thread's part of tile t+1 has landed (AHEAD - 2 tiles may stay in flight)
-    if constexpr (S16)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    vm_wait<(AHEAD - 2) * GL>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage has been read
     asm volatile("" ::: "memory");
@@ -330,12 +330,18 @@ __global__ __launch_bounds__(256, 2) void k_node_gemm(GemmArgs g) {
 int g_node_variant = 0;
 
 hipError_t node_gemm_init() {
-  const void* ks[4] = {(const void*)k_node_gemm<0, false>, (const void*)k_node_gemm<1, false>,
-                       (const void*)k_node_gemm<0, true>, (const void*)k_node_gemm<1, true>};
+  const void* ks[6] = {(const void*)k_node_gemm<0, false, 2>, (const void*)k_node_gemm<1, false, 2>,
+                       (const void*)k_node_gemm<0, true, 2>,  (const void*)k_node_gemm<1, true, 2>,
+                       (const void*)k_node_gemm<0, true, 3>,  (const void*)k_node_gemm<1, true, 3>};
+  constexpr int L3 = STB<true> * NST<true, 3>;
+  const int bytes[6] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, L3, L3};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, NODE_LDS);
+  for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
+
+int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
+constexpr int LDS3 = STB<true> * NST<true, 3>;
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
@@ -350,10 +356,16 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
   }
   const long blocks = ((g.M + NM - 1) / NM) * (g.N / NN);
   const dim3 grid((unsigned)blocks), block(256);
-  if (g.wscale)
-    hipLaunchKernelGGL((g_node_variant == 1 ? k_node_gemm<1, true> : k_node_gemm<0, true>), grid, block, NODE_LDS, s, g);
+  const bool v1 = g_node_variant == 1;
+  // S16: three blocks per CU (3 stages each) once the grid fills a round of them: more waves to hide
+  // the K-loop latency (-7% at M = 40960); small grids keep two blocks and 5 stages
+  const int nb = g_node_blocks ? g_node_blocks : (blocks >= 3 * 256 ? 3 : 2);
+  if (g.wscale && nb == 3)
+    hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3> : k_node_gemm<0, true, 3>), grid, block, LDS3, s, g);
+  else if (g.wscale)
+    hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 2> : k_node_gemm<0, true, 2>), grid, block, NODE_LDS, s, g);
   else
-    hipLaunchKernelGGL((g_node_variant == 1 ? k_node_gemm<1, false> : k_node_gemm<0, false>), grid, block, NODE_LDS, s, g);
+    hipLaunchKernelGGL((v1 ? k_node_gemm<1, false, 2> : k_node_gemm<0, false, 2>), grid, block, NODE_LDS, s, g);
   return hipGetLastError();
 }
 

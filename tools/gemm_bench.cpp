@@ -169,6 +169,21 @@ int main(int argc, char** argv) {
       printf("  split16 k_node_gemm %.1f us %.1f TF (no bias/act %.1f us, no split %.1f us)\n", t16 * 1e3,
              flops / t16 / 1e9, t160 * 1e3, t16v * 1e3);
     }
+    for (int nb : {2, 3}) {
+      g_node_blocks = nb;
+      float tb = time_it(10, s, [&] { CK(node_gemm(g16, s)); });
+      printf("  split16 %d blocks/CU: %.1f us %.1f TF\n", nb, tb * 1e3, flops / tb / 1e9);
+    }
+    g_node_blocks = 3;
+    CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+    g_node_blocks = 0;
+    {
+      std::vector<float> r3((size_t)std::min<long>(M, 4096) * N), r2(r3.size());
+      CK(hipMemcpy(r3.data(), C, r3.size() * 4, hipMemcpyDeviceToHost));
+      CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(r2.data(), C, r2.size() * 4, hipMemcpyDeviceToHost));
+      printf("  3 blocks/CU bit-identical to 2: %s\n", r2 == r3 ? "yes" : "NO");
+    }
     const size_t nc = (size_t)std::min<long>(M, 4096) * N;
     std::vector<float> c1(nc), c2(nc), c3(nc);
     CK(gemm(g, EPI_STD, s)); CK(hipStreamSynchronize(s));  // fp32 MFMA reference
