@@ -265,6 +265,41 @@ def test_decoder_large_ragged_vs_oracle(model1000, cn):
             close(latt[c].cpu(), rl, what=f"{math} lattice c={c}")
 
 
+@pytest.mark.parametrize("lat_scale", [300.0, 3000.0])
+def test_decoder_wide_range_vs_oracle(model1000, cn, lat_scale):
+    """Lattices 300x / 3000x the usual scale (vec(LL^T) up to ~1e8): the lattice term reaches P,
+    S, agg, the node MLP and the residual stream (up to ~1e6 / 1e7 after six layers), far outside
+    fp16's range. The split16 node GEMMs scale each A row by its
+    max (written by the producing kernels), so every arithmetic stays finite and within 1e-4 of
+    the CPU oracle."""
+    nat = [12, 5, 20, 1, 9]
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(29)
+    a = torch.randint(0, 104, (N,), generator=g)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.randn(B, 3, 3, generator=g) * 4 * lat_scale
+    te = model1000.time_embed(torch.full((B,), 700, dtype=torch.long))
+    sd = {k: v.detach().cpu() for k, v in model1000.decoder.state_dict().items()}
+    nat_t = torch.tensor(nat)
+    n2g = torch.arange(B).repeat_interleave(nat_t)
+    hid = []
+    ref = [O.cspnet_forward(sd, default_config(), a, x, lat, nat_t, n2g, te, text.expand(B, -1), hidden=hid)
+           for text in cn]
+    assert max(float(h.abs().max()) for h in hid) > 65504  # the residual stream does leave fp16's range
+    for math in MATHS:
+        model1000.decoder.set_math(math)
+        types, latt, coords, nodes = model1000.decoder.forward_cfg(a.to(DEV), x.to(DEV), lat.to(DEV), nat_t.to(DEV),
+                                                                   te.to(DEV), cn[0].expand(B, -1).to(DEV),
+                                                                   cn[1].expand(B, -1).to(DEV), need_nodes=True)
+        for c in range(2):
+            rt, rl, rc, rh = ref[c]
+            close(nodes[c].cpu(), rh, what=f"{math} nodes c={c} x{lat_scale}")
+            close(types[c].cpu(), rt, what=f"{math} types c={c} x{lat_scale}")
+            close(coords[c].cpu(), rc, what=f"{math} coords c={c} x{lat_scale}")
+            close(latt[c].cpu(), rl, what=f"{math} lattice c={c} x{lat_scale}")
+    model1000.decoder.set_math("split16")
+
+
 @pytest.mark.parametrize("t", [500, 1000])
 def test_math_modes_agree(model1000, cn, t):
     """The GEMM arithmetics agree to fp32 rounding level on 64 x 20, for the
