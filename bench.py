@@ -65,6 +65,9 @@ def parse():
                    "inside the captured step graph (their GEMM epilogues then overlap each other's matrix work)")
     p.add_argument("--math", choices=["split16", "bf16x3", "f32"], default="split16",
                    help="decoder GEMM arithmetic (both fp32-accurate; see include/chemeleon_hip.h)")
+    p.add_argument("--ragged", action="store_true",
+                   help="SURVEY C4 workload: natoms = randint(1, 81, generator seed 7) per sample (use with "
+                        "--n-samples 2048), ranks split by sum of n^2; not the headline metric")
     return p.parse_args()
 
 
@@ -155,12 +158,21 @@ def main():
     from chemeleon_amd.config import default_config
     from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
 
-    # shard: contiguous sample ranges, 512/N each
+    # shard: contiguous sample ranges, 512/N each (ragged: balanced by sum of n^2)
     total = args.n_samples
-    per = [total // world + (1 if r < total % world else 0) for r in range(world)]
-    g0 = sum(per[:rank])
-    natoms = [args.n_atoms] * per[rank]
-    node_base = g0 * args.n_atoms
+    if args.ragged:
+        from chemeleon_amd.distributed import partition
+        all_nat = torch.randint(1, 81, (total,), generator=torch.Generator().manual_seed(7)).tolist()
+        ranges = partition(all_nat, world)
+        per = [b - a for a, b in ranges]
+        g0 = ranges[rank][0]
+        natoms = all_nat[ranges[rank][0]:ranges[rank][1]]
+        node_base = sum(all_nat[:g0])
+    else:
+        per = [total // world + (1 if r < total % world else 0) for r in range(world)]
+        g0 = sum(per[:rank])
+        natoms = [args.n_atoms] * per[rank]
+        node_base = g0 * args.n_atoms
 
     cfg = default_config()
     torch.manual_seed(0)
@@ -229,7 +241,7 @@ def main():
     math = model.decoder.get_math()
     fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
-    traffic, traffic_src = _pmc_traffic(math)
+    traffic, traffic_src = _pmc_traffic(math) if not args.ragged else (None, "not collected for the ragged workload")
     # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
     # = bf16 rate) / 3 products; f32 = the fp32 MFMA peak
     peak = {"bf16x3": BF16X3_PEAK_TFLOPS, "split16": MFMA_BF16_PEAK_TFLOPS / 3}.get(math, MFMA_F32_PEAK_TFLOPS)
@@ -258,7 +270,8 @@ def main():
         print("segment_mean microbench failed:", repr(e), file=sys.stderr)
 
     out = {
-        "metric": "structures/sec (1000-step sample, n_atoms=40)",
+        "metric": ("structures/sec (1000-step sample, n_atoms=40)" if not args.ragged else
+                   "structures/sec (1000-step sample, natoms = randint(1, 81), SURVEY C4)"),
         "value": value,
         "unit": "structures/sec",
         "n_gpus": world,
@@ -271,9 +284,11 @@ def main():
         "dtype": {"f32": "f32", "bf16x3": "f32 (bf16x3-split MFMA, fp32 accumulate)",
                   "split16": "f32 (fp16x2-split edge and node GEMMs with power-of-two row scales, fp32 accumulate)"}[math],
         "data": "synthetic (seeded random-init weights of the real architecture; seeded conditioning vectors)",
-        "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) n_atoms={args.n_atoms}, "
+        "config": {"workload": f"sample n_samples={total} (x{per[rank]}/GPU) "
+                               f"n_atoms={'randint(1,81) seed 7' if args.ragged else args.n_atoms}, "
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
-                   "n_samples": total, "n_atoms": args.n_atoms, "timesteps": T_STEPS,
+                   "n_samples": total, "n_atoms": "ragged 1-80" if args.ragged else args.n_atoms,
+                   "timesteps": T_STEPS,
                    "parallelism": f"sample-sharded x{world}", "noise": "philox (device)",
                    "launch": "eager" if args.no_graph else f"hip graph replay per step, {args.lanes} stream lane(s)"},
         "roofline": {"bound": "mfma",
