@@ -582,8 +582,29 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     if (t < nk - 1) read_frags(0, t + 1, 0);
     mfmas(1);
   }
+  // EPI_SEGMEAN: the epilogue's per-column W scale and bias, one column group ahead (double-buffered
+  // in act() below); the first group is issued here, behind the ring's last loads
+  f32x4 sc[2][4], bb[2][4];
+  auto ld_sb = [&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
+      sc[j & 1][q] = *reinterpret_cast<const f32x4*>(g.wscale + c);
+      bb[j & 1][q] = *reinterpret_cast<const f32x4*>(g.bias + c);
+    }
+  };
   // drain the ring (the tail re-reads still land in LDS) before the epilogue reuses it
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (EPI == EPI_SEGMEAN) {
+    if (!(g.dbg & 128)) {
+      ld_sb(std::integral_constant<int, 0>{});
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // everything but those 8 loads
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
   // EPI_SEGMEAN: the tile's node list {atom count, first row in the tile} for thread tid < nodes,
@@ -634,16 +655,6 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
     // waves at once), then the owners of each 128-column half write it to the tile. The scale and
     // bias vectors are loaded one column group ahead (double-buffered) rather than all up front,
     // which would spill.
-    f32x4 sc[2][4], bb[2][4];
-    auto ld_sb = [&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
-        sc[j & 1][q] = *reinterpret_cast<const f32x4*>(g.wscale + c);
-        bb[j & 1][q] = *reinterpret_cast<const f32x4*>(g.bias + c);
-      }
-    };
     auto act = [&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if constexpr (j < 3) ld_sb(std::integral_constant<int, j + 1>{});
@@ -667,7 +678,6 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
           asm volatile("" : "+v"(acc[i][j][4 * q]), "+v"(acc[i][j][4 * q + 1]), "+v"(acc[i][j][4 * q + 2]),
                        "+v"(acc[i][j][4 * q + 3])::"memory");
     };
-    ld_sb(std::integral_constant<int, 0>{});
     act(std::integral_constant<int, 0>{});
     act(std::integral_constant<int, 1>{});
     act(std::integral_constant<int, 2>{});
