@@ -44,6 +44,15 @@ for k, idx in cu.items():
     gaps.append((ends[-1] - starts[0]) / 100)
 print(f"epilogue time overlapped by another block's main loop on the same CU: {100 * ov / max(tot, 1):.1f}%")
 print(f"CU active span: median {np.median(gaps):.1f} us, min {min(gaps):.1f}, max {max(gaps):.1f}")
+# gap between one block's end marker and the next block's start on the same CU (store drain,
+# wave teardown and dispatch)
+ig = []
+for k, idx in cu.items():
+    idx = sorted(idx, key=lambda i: t0[i])
+    ig += [(t0[b] - te[a_]) / 100 for a_, b in zip(idx, idx[1:]) if t0[b] > te[a_]]
+if ig:
+    print(f"inter-block gap on a CU: median {np.median(ig):.1f} us, p10 {np.percentile(ig, 10):.1f}, "
+          f"p90 {np.percentile(ig, 90):.1f} ({len(ig)} gaps)")
 # first-round phase offset between co-resident blocks
 k0 = sorted(cu)[0]
 for k in sorted(cu)[:3]:
