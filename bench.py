@@ -57,8 +57,11 @@ def parse():
     p.add_argument("--n-atoms", type=int, default=40)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-samples", type=int, default=8)
-    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--cpu-samples", type=int, default=64)
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--no-api-legs", action="store_true",
+                   help="skip the legs that time Chemeleon.sample() end to end (1000 steps, perf mode) and the "
+                        "parity-mode (noise='torch') step")
     p.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
                    "captured HIP graph of the reverse step")
     p.add_argument("--lanes", type=int, default=1, help="concurrent sample groups per GPU, each on its own stream "
@@ -84,12 +87,38 @@ def decoder_pair_flops(natoms, P=2, share_fourier=True):
     return edge + node + heads
 
 
+def host_cores():
+    """CPU cores this process may use: the affinity mask, capped by the cgroup CPU quota (a GPU
+    box shows all of the machine's CPUs in os.cpu_count() but grants one GPU's share), and by the
+    physical core count when SMT siblings are visible (lscpu's cores x sockets)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"affinity {n}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            if q < n:
+                n, how = q, how + f", cgroup quota {q}"
+    except (OSError, ValueError):
+        pass
+    try:
+        import subprocess
+        info = dict(line.split(":", 1) for line in subprocess.run(["lscpu"], capture_output=True, text=True,
+                                                                  timeout=10).stdout.splitlines() if ":" in line)
+        phys = int(info["Core(s) per socket"]) * int(info["Socket(s)"])
+        if phys < n:
+            n, how = phys, how + f", physical cores {phys}"
+    except Exception:  # noqa: BLE001
+        pass
+    return n, how
+
+
 def cpu_baseline(n_samples, n_atoms, steps):
     """Time the oracle (CPU restatement of the reference path) on this host."""
     from chemeleon_amd.config import default_config
     from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
     from oracle import chemeleon_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, how = host_cores()
     torch.set_num_threads(threads)
     cfg = default_config()
     torch.manual_seed(0)
@@ -114,8 +143,44 @@ def cpu_baseline(n_samples, n_atoms, steps):
         dt = (time.perf_counter() - t0) / steps
     return {"value": n_samples / (dt * T_STEPS), "unit": "structures/sec", "cores": threads, "kind": "port",
             "sample": f"oracle (torch CPU restatement of the reference path) {n_samples}x{n_atoms} atoms, "
-                      f"{steps} timed reverse steps after 1 warm-up, {dt:.2f} s/step, extrapolated x{T_STEPS}",
+                      f"{steps} timed reverse steps after 1 warm-up, {dt:.2f} s/step, extrapolated x{T_STEPS}; "
+                      f"{threads} torch threads ({how})",
             "s_per_step": dt}
+
+
+def api_legs(model, n_samples, n_atoms, cond, null, seed, headline):
+    """What a drop-in caller gets (reference chemeleon.py:469-490): Chemeleon.sample() end to end
+    in perf mode (one captured HIP graph replayed per timestep, device Philox noise), including
+    graph capture, the final device->host copy and get_atoms; and the per-step cost of the
+    parity mode (noise='torch': the reference's CPU RNG stream drawn and uploaded every step,
+    eager launches)."""
+    out = {}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    atoms = model.sample(None, n_atoms, n_samples, 2.0, 1e-5, noise="philox", seed=seed, text_embeds=cond,
+                         null_text_embeds=null)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert len(atoms) == n_samples
+    out["sample_philox_graph"] = {"value": n_samples / dt, "unit": "structures/sec", "seconds": dt,
+                                  "ratio_to_headline": (n_samples / dt) / headline,
+                                  "call": f"Chemeleon.sample(n_atoms={n_atoms}, n_samples={n_samples}, "
+                                          "noise='philox') incl. graph capture and get_atoms"}
+    it = model.sample_states([n_atoms] * n_samples, None, 2.0, 1e-5, noise="torch", text_embeds=cond,
+                             null_text_embeds=null, clone=False)
+    next(it)
+    next(it)  # warm-up step
+    torch.cuda.synchronize()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        next(it)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    it.close()
+    out["torch_noise_step"] = {"ms_per_step": ms, "structures_per_sec": n_samples / (ms * 1e-3 * T_STEPS),
+                               "note": "noise='torch' (parity mode): host RNG draw + upload per step, eager launches"}
+    return out
 
 
 def _pmc_traffic(math):
@@ -147,10 +212,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    # (CHM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks sharing one GPU)
+    # One process per GPU. The device is LOCAL_RANK modulo the visible GPUs (the identity on an
+    # 8-GPU node); CHM_DIST_BACKEND=gloo rehearses the same path with several ranks sharing one GPU.
+    # The two backends differ only in init_process_group.
     backend = os.environ.get("CHM_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % torch.cuda.device_count()
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -166,20 +232,24 @@ def main():
     from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
 
     # shard: contiguous sample ranges, 512/N each (ragged: balanced by sum of n^2)
+    from chemeleon_amd.distributed import partition
     total = args.n_samples
     if args.ragged:
-        from chemeleon_amd.distributed import partition
         all_nat = torch.randint(1, 81, (total,), generator=torch.Generator().manual_seed(7)).tolist()
-        ranges = partition(all_nat, world)
-        per = [b - a for a, b in ranges]
-        g0 = ranges[rank][0]
-        natoms = all_nat[ranges[rank][0]:ranges[rank][1]]
-        node_base = sum(all_nat[:g0])
     else:
-        per = [total // world + (1 if r < total % world else 0) for r in range(world)]
-        g0 = sum(per[:rank])
-        natoms = [args.n_atoms] * per[rank]
-        node_base = g0 * args.n_atoms
+        all_nat = [args.n_atoms] * total
+    ranges = partition(all_nat, world)
+    per = [b - a for a, b in ranges]
+    g0 = ranges[rank][0]
+    natoms = all_nat[ranges[rank][0]:ranges[rank][1]]
+    node_base = sum(all_nat[:g0])
+    # initial noise of the whole job from one seeded generator, sliced per rank (with the
+    # global-index Philox keys the result is then independent of the rank count)
+    gen = torch.Generator().manual_seed(args.seed)
+    mask = torch.tensor([[1, 0, 1], [1, 1, 1], [0, 0, 1]]).bool()
+    l_init = torch.randn(total, 3, 3, generator=gen) * mask
+    x_init = torch.randn(sum(all_nat), 3, generator=gen)
+    init = (l_init[g0:g0 + len(natoms)], x_init[node_base:node_base + sum(natoms)])
 
     cfg = default_config()
     torch.manual_seed(0)
@@ -194,7 +264,7 @@ def main():
 
     model.decoder.set_math(args.math)
     it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
-                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
+                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
                              graph=not args.no_graph, lanes=args.lanes)
     next(it)  # initial state
     # per-kernel HIP-event instrumentation (eager launches only; graph captures are not instrumented)
@@ -219,7 +289,7 @@ def main():
         _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
         it2 = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
                                   null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
-                                  t_stop=998)
+                                  init=init, t_stop=998, graph=False)
         for _ in it2:
             pass
         torch.cuda.synchronize()
@@ -230,7 +300,7 @@ def main():
         elapsed = float(tt.item())
         # finished structures -> every rank (the all-gather of the sampler; outside the timed region)
         from chemeleon_amd.distributed import gather_states
-        gather_states(state[1:], natoms)
+        gather_states(state[1:], natoms, natoms_all=[all_nat[a:b] for a, b in ranges])
 
     s_per_step = elapsed / args.steps
     value = total / (s_per_step * T_STEPS)
@@ -331,6 +401,11 @@ def main():
                  "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_api_legs and not args.ragged:
+        try:
+            out["api"] = api_legs(model, total, args.n_atoms, cond, null, args.seed, value)
+        except Exception as e:  # noqa: BLE001
+            out["api"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_samples, args.n_atoms, args.cpu_steps)

@@ -46,6 +46,12 @@ SIGNATURES = {
     "chm_model_get_math": (c_int, [c_void_p]),
     "chm_batch_create": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, ctypes.POINTER(c_void_p)]),
     "chm_batch_destroy": (None, [c_void_p]),
+    "chm_batch_workspace_bytes": (ctypes.c_size_t, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int]),
+    "chm_batch_create_with_workspace": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, c_void_p,
+                                                ctypes.c_size_t, c_void_p, ctypes.POINTER(c_void_p)]),
+    "chm_debug_philox": (c_int, [c_u64, c_int, c_int, c_i64, c_i64, c_int, c_void_p, c_void_p]),
+    "chm_debug_d3pm_philox": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_u64,
+                                      c_i64, c_void_p, c_void_p]),
     "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
     "chm_batch_num_nodes": (c_i64, [c_void_p]),
     "chm_batch_num_edges": (c_i64, [c_void_p]),

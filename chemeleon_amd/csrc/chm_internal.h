@@ -75,9 +75,7 @@ struct EdgeArgs {
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
-// two-workgroups-per-CU variant (128x256 tiles), EPI_STD / EPI_EDGE, unscaled A
-hipError_t edge_gemm_pp(const EdgeArgs& g, int epi, hipStream_t s);
-hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // microbenchmarks
+hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
@@ -136,6 +134,8 @@ struct StepArgs {
   uint64_t seed; int64_t node_base, graph_base;
 };
 hipError_t step_predictor(const StepArgs& a, hipStream_t s);
+// out[i] = Philox uniform (normal = 0) or normal (normal = 1) of (seed, t, kind, base + i)
+hipError_t philox_fill(uint64_t seed, int t, int kind, int64_t base, long n, int normal, float* out, hipStream_t s);
 hipError_t step_corrector(const StepArgs& a, hipStream_t s);
 hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits, const float* logits2,
                        float w1, float w2, const int64_t* xt, const int64_t* tnode, int t_const, const int* d_t,

@@ -770,204 +770,6 @@ __global__ __launch_bounds__(512, 1) void k_edge_gemm(EdgeArgs g) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Two workgroups per CU ("pp"): 256-thread workgroups, 128x256 output tiles, 4 waves of 64x128
-// (the same per-wave accumulators and epilogue as k_edge_gemm), an 80-KB LDS budget each. With
-// one workgroup per CU the epilogue (SiLU / split VALU, S stores at the chip's ~6 TB/s store
-// rate) runs with the matrix cores idle; two resident workgroups that drift out of phase let one
-// workgroup's epilogue run beside the other's MFMAs (the two waves on a SIMD belong to different
-// workgroups). The price: 1.5x the operand bytes per flop (128-row tiles) and one barrier per 24
-// MFMAs.
-// K-tiles of 16: a row's K-tile is 64 B = hi k0-7 | hi k8-15 | lo k0-7 | lo k8-15 (four 16-B
-// pieces taken from the [K/32][hi 32 | lo 32] split rows); piece p of row r sits at p ^ ((r>>2)&3)
-// (conflict-free fragment reads). Ring: 3 stages of A 8 KB + W 16 KB, two K-tiles in flight.
-// ---------------------------------------------------------------------------
-namespace {
-constexpr int PP_TM = 128, PP_TN = 256, PP_BK = 16, PP_ROWB = 64;
-constexpr int PP_A = PP_TM * PP_ROWB, PP_W = PP_TN * PP_ROWB, PP_STAGE = PP_A + PP_W, PP_NST = 3;
-constexpr int PP_LDS = 80 * 1024;
-}  // namespace
-
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void k_edge_pp(EdgeArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int ntn = g.N / PP_TN;
-  const long bid = remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(bid % ntn) * PP_TN;
-  const long row0 = (bid / ntn) * PP_TM;
-  const long nrows = g.M - row0 < PP_TM ? g.M - row0 : PP_TM;
-  const int K = g.K, nk = K / PP_BK;
-  if (g.stagger > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
-  const unsigned long long t0 = g.trace ? rtime() : 0;
-
-  // ---- glds: instruction q of a wave covers 16 rows (lane L: row (L >> 2), LDS piece L & 3,
-  // logical piece (L & 3) ^ ((L >> 4) & 3)); A rows 32w + 16q (q < 2), W rows 64w + 16q (q < 4)
-  const char* Ab = reinterpret_cast<const char*>(g.A);
-  const char* Wb = reinterpret_cast<const char*>(g.W);
-  const long rowB = (long)K * 4;
-  const int lp = (lane & 3) ^ ((lane >> 4) & 3);
-  const unsigned poff = 16u * (lp & 1) + 64u * (lp >> 1);
-  unsigned aoff[2], woff[4];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = 32 * wave + 16 * q + (lane >> 2);
-    aoff[q] = (unsigned)((r < nrows ? r : (int)nrows - 1) * rowB) + poff;
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) woff[q] = (unsigned)((64 * wave + 16 * q + (lane >> 2)) * rowB) + poff;
-  const char* Ablk = Ab + row0 * rowB;
-  const char* Wblk = Wb + (long)n0 * rowB;
-  auto issue = [&](int t) {
-    const int tt = t < nk ? t : nk - 1;  // past the end: re-read the last tile into an idle stage
-    const long kb = (long)(tt >> 1) * 128 + 32 * (tt & 1);
-    char* st = lds + (t % PP_NST) * PP_STAGE;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(Ablk + kb + aoff[q]), (lds_void*)(st + (32 * wave + 16 * q) * PP_ROWB),
-                                       16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(Wblk + kb + woff[q]),
-                                       (lds_void*)(st + PP_A + (64 * wave + 16 * q) * PP_ROWB), 16, 0, 0);
-  };
-
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-  const int swz = (r32 >> 2) & 3;
-  const int chh = 16 * (h ^ swz), chl = 16 * ((2 + h) ^ swz);  // hi / lo fragment pieces
-  const int fa = (wm * 64 + r32) * PP_ROWB, fw = (wn * 128 + r32) * PP_ROWB;
-
-  // fragments double-buffered across K-tiles: while the MFMAs of tile t run, the fragments of
-  // tile t+1 are read and the loads of tile t+3 are issued, both interleaved between the MFMAs
-  f16x8 fr[2][12];  // [set][ah0 ah1 al0 al1 | wh0..3 | wl0..3]
-  auto read_frags = [&](int set, int t) {
-    const char* st = lds + (t % PP_NST) * PP_STAGE;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      fr[set][i] = *reinterpret_cast<const f16x8*>(st + fa + i * 32 * PP_ROWB + chh);
-      fr[set][2 + i] = *reinterpret_cast<const f16x8*>(st + fa + i * 32 * PP_ROWB + chl);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      fr[set][4 + j] = *reinterpret_cast<const f16x8*>(st + PP_A + fw + j * 32 * PP_ROWB + chh);
-      fr[set][8 + j] = *reinterpret_cast<const f16x8*>(st + PP_A + fw + j * 32 * PP_ROWB + chl);
-    }
-  };
-  issue(0);
-  issue(1);
-  issue(2);
-  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  read_frags(0, 0);
-  // tile t uses fragment set t & 1; the loop is unrolled by two so the sets stay in registers
-  auto step = [&](int t, auto CUR) {
-    constexpr int cur = decltype(CUR)::value;
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // this thread's part of tile t+1 has landed
-    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): tile t's fragments are in
-    __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage is free
-    asm volatile("" ::: "memory");
-    issue(t + 3);                                     // past the end: re-reads into the free stage
-    read_frags(cur ^ 1, t + 1);                       // past the end: reads a re-read tile
-    __builtin_amdgcn_s_setprio(1);
-    // small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][8 + j], fr[cur][i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][4 + j], fr[cur][2 + i], acc[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fr[cur][4 + j], fr[cur][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  for (int t = 0; t < nk; t += 2) {  // nk = K / 16 is even
-    step(t, std::integral_constant<int, 0>{});
-    step(t + 1, std::integral_constant<int, 1>{});
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + n0 + wn * 128 + j * 32 + 8 * q + 4 * h);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] *= sc[e];
-    }
-  if (EPI == EPI_EDGE) {
-    const unsigned long long tm = g.trace ? rtime() : 0;
-    edge_epilogue<4>(g, acc, lds, PP_LDS, wave, lane, row0, nrows, n0);
-    if (g.trace) {
-      __syncthreads();
-      if (tid == 0) {
-        unsigned long long* o = g.trace + 6 * blockIdx.x;
-        o[0] = hwid(); o[1] = t0; o[2] = tm; o[3] = rtime();
-      }
-    }
-    return;
-  }
-  if (!g.C) return;  // (microbenchmark: main loop only)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long lr = wm * 64 + i * 32 + r32;
-    if (lr >= nrows) continue;
-    const long row = row0 + lr;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = n0 + wn * 128 + j * 32 + 8 * q + 4 * h;
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-        *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
-      }
-  }
-}
-
-hipError_t edge_gemm_pp(const EdgeArgs& g, int epi, hipStream_t s) {
-  if (g.N % PP_TN || g.K % 32 || !g.A || !g.W || !g.wscale || g.aexp || g.M <= 0) return hipErrorInvalidValue;
-  if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g))
-    return hipErrorInvalidValue;
-  if (epi != EPI_EDGE && epi != EPI_STD) return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    const void* ks[] = {(const void*)k_edge_pp<EPI_STD>, (const void*)k_edge_pp<EPI_EDGE>};
-    for (const void* k : ks) {
-      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
-      if (e != hipSuccess) return e;
-    }
-    attr = true;
-  }
-  const long blocks = ((g.M + PP_TM - 1) / PP_TM) * (g.N / PP_TN);
-  if (epi == EPI_EDGE)
-    hipLaunchKernelGGL(k_edge_pp<EPI_EDGE>, dim3((unsigned)blocks), dim3(256), PP_LDS, s, g);
-  else
-    hipLaunchKernelGGL(k_edge_pp<EPI_STD>, dim3((unsigned)blocks), dim3(256), PP_LDS, s, g);
-  return hipGetLastError();
-}
-
 hipError_t edge_gemm_init() {
   const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false>, (const void*)k_edge_gemm<EPI_EDGE, false>,
                       (const void*)k_edge_gemm<EPI_SEGMEAN, true>, (const void*)k_edge_gemm<EPI_STD, true>};
@@ -978,6 +780,7 @@ hipError_t edge_gemm_init() {
   return hipSuccess;
 }
 
+#ifdef CHM_MICROBENCH  // (tools/gemm_bench.cpp: main-loop schedule variants)
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s) {
   const void* ks[] = {(const void*)k_edge_gemm<EPI_STD, false, 0>, (const void*)k_edge_gemm<EPI_STD, false, 1>,
                       (const void*)k_edge_gemm<EPI_STD, false, 2>, (const void*)k_edge_gemm<EPI_STD, false, 3>,
@@ -998,6 +801,8 @@ hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s) {
   void* args[] = {&ga};
   return hipLaunchKernel(ks[var], dim3((unsigned)blocks), dim3(512), args, LDS_B, s);
 }
+
+#endif
 
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
   if (g.N % BN || g.K % BK || !g.A || !g.W || !g.wscale) return hipErrorInvalidValue;

@@ -65,6 +65,19 @@ __device__ __forceinline__ float rng_normal(uint64_t seed, int t, int kind, uint
   return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
 }
 
+// the perf-mode streams themselves, for their statistical tests (chm_debug_philox)
+__global__ void k_philox_fill(uint64_t seed, int t, int kind, int64_t base, long n, int normal, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = normal ? rng_normal(seed, t, kind, (uint64_t)(base + i)) : rng_uniform(seed, t, kind, (uint64_t)(base + i));
+}
+hipError_t philox_fill(uint64_t seed, int t, int kind, int64_t base, long n, int normal, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_philox_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seed, t, kind, base, n, normal,
+                     out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // GEMM  C = epi(A . W^T) on fp32 MFMA. 128x128x16 tiles, 4 waves in 2x2, each
 // wave 64x64 = 2x2 v_mfma_f32_32x32x2_f32 accumulators. Within a 16-deep K

@@ -7,8 +7,10 @@
 //              allocate nothing, synchronise nothing and are capturable.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,7 +61,6 @@ struct chm_model {
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
-  int edge1_pp = 0;      // CHM_EDGE1_PP: edge layer 1 on the two-workgroups-per-CU kernel
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
@@ -82,7 +83,7 @@ struct chm_batch {
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
   float* rmx;        // split16 node GEMMs: the four row-max arrays [4][P*N] (RMX_*)
   unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
-  std::vector<void*> allocs;
+  void* owned = nullptr;  // the library's own allocation (chm_batch_create); null for caller workspaces
   size_t bytes = 0;
 };
 
@@ -226,8 +227,6 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (ng) m->node_glds = atoi(ng);
     const char* n16 = getenv("CHM_NODE16");
     if (n16) m->node16 = atoi(n16);
-    const char* pp = getenv("CHM_EDGE1_PP");
-    if (pp) m->edge1_pp = atoi(pp);
     m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
     if (tl) m->edge_trace_layer = atoi(tl);
@@ -332,87 +331,110 @@ extern "C" void chm_model_destroy(chm_model* m) {
   delete m;
 }
 
-extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, chm_batch** out) {
-  if (!out) return fail(CHM_E_ARG, "out is NULL");
-  *out = nullptr;
-  if (!m || !h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
-  if (max_pairs < 1 || max_pairs > 2) return fail(CHM_E_ARG, "max_pairs must be 1 or 2");
-  std::vector<int> nat(h_natoms, h_natoms + B), noff(B + 1), n2g;
-  std::vector<long> eoff(B + 1);
+// Host-side index tables of a batch (the implicit fc edge layout) and the byte layout of its
+// device memory: index tables first, then the decoder workspace, each piece 256-byte aligned.
+// The same carve() sequence sizes the block (base == null) and binds a batch to it.
+struct BatchTables {
+  std::vector<int> nat, noff, n2g, ei, ej, nn;
+  std::vector<long> eoff, estart;
+  std::vector<int2> tiles;
+  long N = 0, E = 0;
+};
+
+static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t) {
+  t.nat.assign(h_natoms, h_natoms + B);
+  t.noff.assign(B + 1, 0);
+  t.eoff.assign(B + 1, 0);
   long N = 0, E = 0;
   for (int g = 0; g < B; ++g) {
-    if (nat[g] < 1) return fail(CHM_E_ARG, "every crystal needs at least one atom");
-    noff[g] = (int)N;
-    eoff[g] = E;
-    N += nat[g];
-    E += (long)nat[g] * nat[g];
+    if (t.nat[g] < 1) return fail(CHM_E_ARG, "every crystal needs at least one atom");
+    if (t.nat[g] > kTileRows) return fail(CHM_E_UNSUPPORTED, "crystals above 256 atoms are not supported");
+    t.noff[g] = (int)N;
+    t.eoff[g] = E;
+    N += t.nat[g];
+    E += (long)t.nat[g] * t.nat[g];
+    if (N > (1L << 30) || E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
   }
-  noff[B] = (int)N;
-  eoff[B] = E;
-  if (N > (1L << 30) || E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
-  n2g.resize(N);
-  std::vector<int> ei(E), ej(E);
+  t.noff[B] = (int)N;
+  t.eoff[B] = E;
+  t.N = N;
+  t.E = E;
+  return CHM_OK;
+}
+
+// fills the per-node / per-edge tables (only when the batch is really built)
+static void batch_fill(BatchTables& t) {
+  const int B = (int)t.nat.size();
+  const long N = t.N, E = t.E;
+  t.n2g.resize(N);
+  t.ei.resize(E);
+  t.ej.resize(E);
+  t.nn.resize(N);
+  t.estart.resize(N);
   for (int g = 0; g < B; ++g) {
-    for (int i = 0; i < nat[g]; ++i) n2g[noff[g] + i] = g;
-    long e = eoff[g];
-    for (int i = 0; i < nat[g]; ++i)
-      for (int j = 0; j < nat[g]; ++j, ++e) {
-        ei[e] = noff[g] + i;
-        ej[e] = noff[g] + j;
+    for (int i = 0; i < t.nat[g]; ++i) {
+      t.n2g[t.noff[g] + i] = g;
+      t.nn[t.noff[g] + i] = t.nat[g];
+    }
+    long e = t.eoff[g];
+    for (int i = 0; i < t.nat[g]; ++i)
+      for (int j = 0; j < t.nat[g]; ++j, ++e) {
+        t.ei[e] = t.noff[g] + i;
+        t.ej[e] = t.noff[g] + j;
       }
   }
-  std::vector<long> estart(N);
-  std::vector<int2> tiles;
-  {
-    int cur0 = 0;
-    long rows = 0;
-    for (int g = 0; g < B; ++g)
-      for (int i = 0; i < nat[g]; ++i) {
-        const int node = noff[g] + i;
-        estart[node] = eoff[g] + (long)i * nat[g];
-        if (nat[g] > kTileRows) return fail(CHM_E_UNSUPPORTED, "crystals above 256 atoms are not supported");
-        if (rows + nat[g] > kTileRows) {
-          tiles.push_back(make_int2(cur0, node));
-          cur0 = node;
-          rows = 0;
-        }
-        rows += nat[g];
+  // segment tiles: runs of whole nodes whose edge rows fit one 256-row GEMM tile
+  int cur0 = 0;
+  long rows = 0;
+  t.tiles.clear();
+  for (int g = 0; g < B; ++g)
+    for (int i = 0; i < t.nat[g]; ++i) {
+      const int node = t.noff[g] + i;
+      t.estart[node] = t.eoff[g] + (long)i * t.nat[g];
+      if (rows + t.nat[g] > kTileRows) {
+        t.tiles.push_back(make_int2(cur0, node));
+        cur0 = node;
+        rows = 0;
       }
-    tiles.push_back(make_int2(cur0, (int)N));
-  }
-  chm_batch* b = new chm_batch();
-  b->m = m;
-  b->math = m->math;
-  b->B = B;
-  b->P = max_pairs;
-  b->N = N;
-  b->E = E;
-  b->h_natoms = nat;
-  const int P = max_pairs, L = m->d.num_layers, X = m->d.text_dim;
-  auto alloc = [&](size_t bytes) -> void* {
-    void* ptr = nullptr;
-    if (hipMalloc(&ptr, bytes < 256 ? 256 : bytes) != hipSuccess) return nullptr;
-    b->allocs.push_back(ptr);
-    b->bytes += bytes;
-    return ptr;
+      rows += t.nat[g];
+    }
+  t.tiles.push_back(make_int2(cur0, (int)N));
+}
+
+// number of segment tiles without building the tables (sizing only)
+static long count_tiles(const BatchTables& t) {
+  long n = 1, rows = 0;
+  for (size_t g = 0; g < t.nat.size(); ++g)
+    for (int i = 0; i < t.nat[g]; ++i) {
+      if (rows + t.nat[g] > kTileRows) {
+        ++n;
+        rows = 0;
+      }
+      rows += t.nat[g];
+    }
+  return n;
+}
+
+// carves every device buffer of `b` from `base` (null: sizing pass); returns the bytes used
+static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long ntiles) {
+  const int P = b->P, L = m->d.num_layers, X = m->d.text_dim, B = b->B;
+  const long N = b->N, E = b->E;
+  size_t off = 0;
+  auto carve = [&](size_t bytes) -> void* {
+    const size_t o = off;
+    off += (bytes + 255) / 256 * 256;
+    return base ? base + o : nullptr;
   };
-  bool ok = true;
-  auto fl = [&](size_t n) {
-    float* ptr = (float*)alloc(n * sizeof(float));
-    ok = ok && ptr;
-    return ptr;
-  };
-  b->natoms = (int*)alloc(B * sizeof(int));
-  b->node_off = (int*)alloc((B + 1) * sizeof(int));
-  b->edge_off = (long*)alloc((B + 1) * sizeof(long));
-  b->n2g = (int*)alloc(N * sizeof(int));
-  b->ei = (int*)alloc(E * sizeof(int));
-  b->ej = (int*)alloc(E * sizeof(int));
-  b->node_estart = (long*)alloc(N * sizeof(long));
-  b->node_n = (int*)alloc(N * sizeof(int));
-  b->tiles = (int2*)alloc(tiles.size() * sizeof(int2));
-  b->ntiles = (int)tiles.size();
-  ok = b->node_n && b->natoms && b->node_off && b->edge_off && b->n2g && b->ei && b->ej && b->node_estart && b->tiles;
+  auto fl = [&](size_t n) { return (float*)carve(n * sizeof(float)); };
+  b->natoms = (int*)carve(B * sizeof(int));
+  b->node_off = (int*)carve((B + 1) * sizeof(int));
+  b->edge_off = (long*)carve((B + 1) * sizeof(long));
+  b->n2g = (int*)carve(N * sizeof(int));
+  b->ei = (int*)carve(E * sizeof(int));
+  b->ej = (int*)carve(E * sizeof(int));
+  b->node_estart = (long*)carve(N * sizeof(long));
+  b->node_n = (int*)carve(N * sizeof(int));
+  b->tiles = (int2*)carve(ntiles * sizeof(int2));
   b->cin = fl((size_t)P * B * (TD + X));
   b->cemb = fl((size_t)P * B * 2 * H);
   b->Hres = fl((size_t)P * N * H);
@@ -430,24 +452,56 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
   b->LAT = fl((size_t)P * B * 9);
-  if (!ok) {
-    chm_batch_destroy(b);
-    return fail(CHM_E_HIP, "hipMalloc failed for batch workspace");
+  return off;
+}
+
+static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, void* d_ws,
+                       size_t ws_bytes, hipStream_t s, chm_batch** out) {
+  if (!out) return fail(CHM_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (!m || !h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
+  if (max_pairs < 1 || max_pairs > 2) return fail(CHM_E_ARG, "max_pairs must be 1 or 2");
+  BatchTables t;
+  int rc = batch_tables(h_natoms, B, t);
+  if (rc) return rc;
+  batch_fill(t);
+  chm_batch* b = new chm_batch();
+  b->m = m;
+  b->math = m->math;
+  b->B = B;
+  b->P = max_pairs;
+  b->N = t.N;
+  b->E = t.E;
+  b->h_natoms = t.nat;
+  b->ntiles = (int)t.tiles.size();
+  const size_t need = batch_layout(b, m, nullptr, b->ntiles);
+  char* base = (char*)d_ws;
+  if (!base) {
+    if (hipMalloc(&b->owned, need) != hipSuccess) {
+      delete b;
+      return fail(CHM_E_HIP, "hipMalloc failed for the batch workspace (" + std::to_string(need) + " bytes)");
+    }
+    base = (char*)b->owned;
+  } else if (ws_bytes < need || ((uintptr_t)base & 255)) {
+    delete b;
+    return fail(CHM_E_ARG, "workspace too small or not 256-byte aligned (need " + std::to_string(need) + " bytes)");
   }
+  b->bytes = batch_layout(b, m, base, b->ntiles);
+  // index tables (setup only: the host vectors must outlive the copies, so the stream is drained)
   hipError_t e = hipSuccess;
-  if (e == hipSuccess) e = hipMemcpy(b->natoms, nat.data(), B * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->node_off, noff.data(), (B + 1) * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->edge_off, eoff.data(), (B + 1) * sizeof(long), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->n2g, n2g.data(), N * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->ei, ei.data(), E * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->ej, ej.data(), E * sizeof(int), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(b->node_estart, estart.data(), N * sizeof(long), hipMemcpyHostToDevice);
-  if (e == hipSuccess) {
-    std::vector<int> nn(N);
-    for (long i = 0; i < N; ++i) nn[i] = nat[n2g[i]];
-    e = hipMemcpy(b->node_n, nn.data(), N * sizeof(int), hipMemcpyHostToDevice);
-  }
-  if (e == hipSuccess) e = hipMemcpy(b->tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
+  auto up = [&](void* dst, const void* src, size_t bytes) {
+    if (e == hipSuccess && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s);
+  };
+  up(b->natoms, t.nat.data(), B * sizeof(int));
+  up(b->node_off, t.noff.data(), (B + 1) * sizeof(int));
+  up(b->edge_off, t.eoff.data(), (B + 1) * sizeof(long));
+  up(b->n2g, t.n2g.data(), t.N * sizeof(int));
+  up(b->ei, t.ei.data(), t.E * sizeof(int));
+  up(b->ej, t.ej.data(), t.E * sizeof(int));
+  up(b->node_estart, t.estart.data(), t.N * sizeof(long));
+  up(b->node_n, t.nn.data(), t.N * sizeof(int));
+  up(b->tiles, t.tiles.data(), t.tiles.size() * sizeof(int2));
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     chm_batch_destroy(b);
     return fail(CHM_E_HIP, std::string("index upload: ") + hipGetErrorString(e));
@@ -456,9 +510,37 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   return CHM_OK;
 }
 
+extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, chm_batch** out) {
+  return batch_build(m, h_natoms, B, max_pairs, nullptr, 0, nullptr, out);
+}
+
+extern "C" size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs) {
+  if (!m || !h_natoms || B < 1 || max_pairs < 1 || max_pairs > 2) {
+    fail(CHM_E_ARG, "bad batch arguments");
+    return 0;
+  }
+  BatchTables t;
+  if (batch_tables(h_natoms, B, t)) return 0;
+  chm_batch b;
+  b.m = m;
+  b.math = m->math;
+  b.B = B;
+  b.P = max_pairs;
+  b.N = t.N;
+  b.E = t.E;
+  return batch_layout(&b, m, nullptr, count_tiles(t));
+}
+
+extern "C" int chm_batch_create_with_workspace(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs,
+                                               void* d_workspace, size_t workspace_bytes, void* stream,
+                                               chm_batch** out) {
+  if (!d_workspace) return fail(CHM_E_ARG, "workspace is NULL");
+  return batch_build(m, h_natoms, B, max_pairs, d_workspace, workspace_bytes, (hipStream_t)stream, out);
+}
+
 extern "C" void chm_batch_destroy(chm_batch* b) {
   if (!b) return;
-  for (void* p : b->allocs) (void)hipFree(p);
+  if (b->owned) (void)hipFree(b->owned);
   delete b;
 }
 
@@ -470,6 +552,7 @@ extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -
 namespace {
 struct ProfRec { int id; hipEvent_t a, b; };
 bool g_prof_on = false;
+std::mutex g_prof_mu;
 std::vector<hipEvent_t> g_pool;
 std::vector<ProfRec> g_recs;
 size_t g_pool_next = 0;
@@ -478,7 +561,9 @@ constexpr size_t kPoolPairs = 8192;
 struct ProfScope {
   int id; hipStream_t s; hipEvent_t b = nullptr;
   ProfScope(int id_, hipStream_t s_) : id(id_), s(s_) {
-    if (!g_prof_on || g_pool_next + 2 > g_pool.size()) return;
+    if (!g_prof_on) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (g_pool_next + 2 > g_pool.size()) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;  // not in graphs
     hipEvent_t a = g_pool[g_pool_next++];
@@ -491,6 +576,7 @@ struct ProfScope {
 }  // namespace
 
 extern "C" int chm_prof_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
   if (on && g_pool.empty()) {
     g_pool.resize(2 * kPoolPairs);
     for (auto& e : g_pool)
@@ -501,6 +587,7 @@ extern "C" int chm_prof_enable(int on) {
 }
 
 extern "C" int chm_prof_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
   g_recs.clear();
   g_pool_next = 0;
   return CHM_OK;
@@ -508,6 +595,7 @@ extern "C" int chm_prof_reset(void) {
 
 extern "C" int chm_prof_read(int kernel, int64_t* launches, double* total_ms) {
   if (!launches || !total_ms) return fail(CHM_E_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(g_prof_mu);
   int64_t n = 0;
   double tot = 0;
   for (const auto& r : g_recs) {
@@ -555,7 +643,7 @@ static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const v
 // 1 or 2 records {hw id, t0, t_mainloop, t_end, ...} per block (s_memrealtime), dumped to the file
 template <class F>
 static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which, long E, hipStream_t s, F&& launch) {
-  static int traced = 0;
+  static std::atomic<int> traced{0};
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
   const bool tr = m->edge_trace && m->edge_trace_layer == which && traced < 4 &&
                   hipStreamIsCapturing(s, &cst) == hipSuccess && cst == hipStreamCaptureStatusNone && ++traced == 4;
@@ -635,7 +723,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
         HIPCHK(traced_edge_launch(m, ea, 1, E, s, [&] {
-          return m->edge1_pp ? edge_gemm_pp(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s);
+          return edge_gemm(ea, EPI_EDGE, s);
         }));
       }
       {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
@@ -778,6 +866,24 @@ extern "C" int chm_d3pm_sample(int N, int A, int T, const float* logits, const i
   if (N == 0) return CHM_OK;
   if (!logits || !xt || !tn || !noise || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
   HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, noise, q1, qm, out, 0, 0,
+                     (hipStream_t)stream));
+  return CHM_OK;
+}
+
+extern "C" int chm_debug_philox(uint64_t seed, int t, int kind, int64_t base, int64_t n, int normal, float* out,
+                                void* stream) {
+  if (n < 0 || !out || kind < 0 || kind > 3) return fail(CHM_E_ARG, "bad arguments");
+  HIPCHK(philox_fill(seed, t, kind, base, n, normal, out, (hipStream_t)stream));
+  return CHM_OK;
+}
+
+extern "C" int chm_debug_d3pm_philox(int N, int A, int T, const float* logits, const int64_t* xt, const int64_t* tn,
+                                     const float* q1, const float* qm, uint64_t seed, int64_t node_base, int64_t* out,
+                                     void* stream) {
+  if (N < 0 || A < 1 || A > 128 || T < 1) return fail(CHM_E_ARG, "bad sizes");
+  if (N == 0) return CHM_OK;
+  if (!logits || !xt || !tn || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
+  HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, nullptr, q1, qm, out, seed, node_base,
                      (hipStream_t)stream));
   return CHM_OK;
 }

@@ -23,10 +23,12 @@ import torch.distributed as dist
 
 def partition(natoms: Sequence[int], world: int) -> List[Tuple[int, int]]:
     """Contiguous [g0, g1) crystal ranges per rank with roughly equal sum of
-    n^2 (the fc edge work). Every rank gets at least one crystal when
-    len(natoms) >= world."""
+    n^2 (the fc edge work). Every rank gets at least one crystal; fewer
+    crystals than ranks is an error."""
     natoms = [int(n) for n in natoms]
     G = len(natoms)
+    if G < max(world, 1):
+        raise ValueError(f"{G} crystals cannot be sharded over {world} ranks (one crystal at least per rank)")
     if world <= 1:
         return [(0, G)]
     w = [n * n for n in natoms]
@@ -55,26 +57,39 @@ def broadcast_conditioning(cond: torch.Tensor, null: torch.Tensor, src: int = 0,
 
 
 def gather_states(states: Tuple[torch.Tensor, torch.Tensor, torch.Tensor], natoms_local: Sequence[int],
-                  group=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, List[int]]:
+                  group=None, natoms_all: Optional[Sequence[Sequence[int]]] = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, List[int]]:
     """All-gather (atom_types [N_r], frac [N_r,3], lattices [B_r,3,3]) from
     every rank, padding to the largest shard. Returns the concatenated global
-    tensors (rank order) and the global natoms list."""
+    tensors (rank order) and the global natoms list.
+
+    natoms_all (every rank's crystal list, e.g. from `partition` of a global
+    list all ranks hold) skips the size exchange: then the gather is exactly
+    three collectives and no host synchronisation. Without it the sizes are
+    exchanged first (two small all-gathers, one host read each)."""
     a, x, lat = states
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return a, x, lat, list(natoms_local)
     world = dist.get_world_size(group)
     dev = x.device
-    nl = torch.tensor([len(natoms_local)], device=dev, dtype=torch.long)
-    counts = [torch.zeros_like(nl) for _ in range(world)]
-    dist.all_gather(counts, nl, group=group)
-    counts = [int(c.item()) for c in counts]
+    if natoms_all is None:
+        nl = torch.tensor([len(natoms_local)], device=dev, dtype=torch.long)
+        counts = [torch.zeros_like(nl) for _ in range(world)]
+        dist.all_gather(counts, nl, group=group)
+        counts = torch.cat(counts).tolist()
+        bmax = max(counts)
+        nat = torch.zeros(bmax, device=dev, dtype=torch.long)
+        nat[:len(natoms_local)] = torch.tensor(list(natoms_local), device=dev)
+        nats = [torch.zeros_like(nat) for _ in range(world)]
+        dist.all_gather(nats, nat, group=group)
+        rows = torch.stack(nats).tolist()
+        natoms_all = [rows[r][:counts[r]] for r in range(world)]
+    natoms_all = [[int(n) for n in ns] for ns in natoms_all]
+    if len(natoms_all) != world:
+        raise ValueError("natoms_all must hold one crystal list per rank")
+    counts = [len(ns) for ns in natoms_all]
     bmax = max(counts)
-    nat = torch.zeros(bmax, device=dev, dtype=torch.long)
-    nat[:len(natoms_local)] = torch.tensor(list(natoms_local), device=dev)
-    nats = [torch.zeros_like(nat) for _ in range(world)]
-    dist.all_gather(nats, nat, group=group)
-    nats = [nats[r][:counts[r]].tolist() for r in range(world)]
-    nmax = max(sum(n) for n in nats)
+    nmax = max(sum(ns) for ns in natoms_all)
 
     def pad(t, rows):
         out = torch.zeros((rows,) + tuple(t.shape[1:]), device=dev, dtype=t.dtype)
@@ -87,10 +102,10 @@ def gather_states(states: Tuple[torch.Tensor, torch.Tensor, torch.Tensor], natom
         buf = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(buf, p, group=group)
         res.append(buf)
-    A = torch.cat([res[0][r][:sum(nats[r])] for r in range(world)])
-    X = torch.cat([res[1][r][:sum(nats[r])] for r in range(world)])
+    A = torch.cat([res[0][r][:sum(natoms_all[r])] for r in range(world)])
+    X = torch.cat([res[1][r][:sum(natoms_all[r])] for r in range(world)])
     LT = torch.cat([res[2][r][:counts[r]] for r in range(world)])
-    return A, X, LT, [n for ns in nats for n in ns]
+    return A, X, LT, [n for ns in natoms_all for n in ns]
 
 
 @torch.no_grad()
@@ -103,7 +118,11 @@ def sample_distributed(model, natoms: Sequence[int], cond: torch.Tensor, null: t
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     natoms = [int(n) for n in natoms]
-    g0, g1 = partition(natoms, world)[rank]
+    # every rank holds the same list, so every rank raises here, before any collective
+    if len(natoms) < world:
+        raise ValueError(f"{len(natoms)} crystals cannot be sharded over {world} ranks (one crystal at least per rank)")
+    ranges = partition(natoms, world)
+    g0, g1 = ranges[rank]
     cond, null = broadcast_conditioning(cond.to(model.device), null.to(model.device), 0, group)
     if cond.shape[0] == len(natoms):
         cond, null = cond[g0:g1], null[g0:g1]
@@ -120,4 +139,4 @@ def sample_distributed(model, natoms: Sequence[int], cond: torch.Tensor, null: t
                                     null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
                                     init=(l0[g0:g1], x0[node_base:node_base + sum(local)])):
         pass
-    return gather_states(last[1:], local, group)
+    return gather_states(last[1:], local, group, natoms_all=[natoms[r0:r1] for r0, r1 in ranges])

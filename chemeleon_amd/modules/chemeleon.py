@@ -115,8 +115,18 @@ class Chemeleon(nn.Module):
             raise RuntimeError(f"checkpoint mismatch: missing {missing}, unexpected {unexpected}")
         if m.text_encoder is not None and isinstance(m.text_encoder, nn.Module):
             te = {k[len("text_encoder."):]: v for k, v in sd.items() if k.startswith("text_encoder.")}
-            if te:
-                m.text_encoder.load_state_dict(te, strict=False)
+            te_missing, te_unexpected = m.text_encoder.load_state_dict(te, strict=False)
+            # the frozen language model (and a CrystalCLIP's own copy of it) is sourced from the local
+            # model directory, and the CrystalCLIP graph side is training / retrieval only; everything
+            # trained with the sampler (text_emb.*, null_text_embeds, the CLIP projection) must come
+            # from the checkpoint
+            frozen = ("text_encoder.", "clip_model.text_encoder.", "clip_model.graph_encoder.",
+                      "clip_model.graph_proj.")
+            te_missing = [k for k in te_missing if not k.startswith(frozen)]
+            te_unexpected = [k for k in te_unexpected if not k.startswith(frozen)]
+            if strict and (te_missing or te_unexpected):
+                raise RuntimeError(f"checkpoint text-encoder mismatch: missing {te_missing}, "
+                                   f"unexpected {te_unexpected}")
         return m
 
     @classmethod
@@ -142,9 +152,12 @@ class Chemeleon(nn.Module):
         expressions (chemeleon.py:413-457) on the host, once; plus the
         time-embedding table (cspnet.py:28-35). Returns (chm_schedule, keepalive)."""
         dev = self.device
-        key = (str(dev), float(step_lr))
+        bufs = [b for mod in (self.beta_scheduler, self.sigma_scheduler, self.d3pm) for b in mod.buffers()]
+        key = (str(dev), float(step_lr), tuple((b.data_ptr(), b._version) for b in bufs))
         if key in self._tables:
             return self._tables[key]
+        if len(self._tables) >= 4:
+            self._tables.pop(next(iter(self._tables)))
         T = self.num_timesteps
         bs, ss = self.beta_scheduler, self.sigma_scheduler
         al_, ac_, sg_ = bs.alphas.cpu(), bs.alphas_cumprod.cpu(), bs.sigmas.cpu()
@@ -204,14 +217,22 @@ class Chemeleon(nn.Module):
                       text_embeds=None, null_text_embeds=None, clone: bool = True, t_stop: int = 0,
                       node_base: int = 0, graph_base: int = 0,
                       init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                      graph: bool = False, lanes: int = 1) -> Iterator[Tuple]:
+                      graph: Optional[bool] = None, lanes: int = 1) -> Iterator[Tuple]:
         """Reverse loop of chemeleon.py:305-467 yielding device tensors
         (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
         starting with the pure-noise state at t = T.
 
-        graph=True (noise="philox" only): one reverse step is captured once
-        as a HIP graph (chm_sample_step_dt reads t from device memory and
-        decrements it) and replayed for every timestep.
+        graph=True (noise="philox" only; the default in that mode): one reverse
+        step is captured once as a HIP graph (chm_sample_step_dt reads t from
+        device memory and decrements it) and replayed for every timestep.
+
+        Initial noise: from `init` = (l_T [B,3,3], x_T [N,3]) if given, else drawn
+        on the CPU from the global generator (noise="torch", chemeleon.py:348-349)
+        or from Generator(seed) (noise="philox") for THIS batch. The per-step
+        Philox noise is keyed by global node / graph index (node_base,
+        graph_base), so a shard reproduces its crystals of a larger run exactly
+        when it is also given that run's initial noise for them (init=, as
+        sample_distributed does).
 
         lanes > 1 (graph mode): the crystals are split into that many contiguous
         groups of similar edge work, each stepped on its own stream inside the
@@ -229,6 +250,8 @@ class Chemeleon(nn.Module):
             raise ValueError("natoms and texts must have the same number of elements.")
         if noise not in ("torch", "philox"):
             raise ValueError("noise must be 'torch' or 'philox'")
+        if graph is None:
+            graph = noise == "philox"
         dev = self.device
         if dev.type != "cuda":
             raise RuntimeError("Chemeleon (chemeleon_amd) samples on a HIP device only; call .to('cuda') first")
@@ -264,9 +287,11 @@ class Chemeleon(nn.Module):
             noff = [0]
             for n in natoms:
                 noff.append(noff[-1] + n)
-            # per-lane workspaces are created before the capture (allocation is not capturable)
-            lane_batches = [batch if len(groups) == 1 else self.decoder.hip_batch(natoms[g0:g1], max_pairs=2)
-                            for g0, g1 in groups]
+            # per-lane workspaces are created before the capture (allocation is not capturable); each
+            # lane runs concurrently with the others, so each gets its own (never the shared cache entry,
+            # which two lanes of identical crystal lists would otherwise both receive)
+            lane_batches = [batch] if len(groups) == 1 else [
+                self.decoder.hip_batch(natoms[g0:g1], max_pairs=2, private=True) for g0, g1 in groups]
             hg = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
             lane_streams = [torch.cuda.Stream(device=dev) for _ in groups[1:]]
@@ -309,7 +334,8 @@ class Chemeleon(nn.Module):
 
     @torch.no_grad()
     def reverse_step(self, t: int, atom_types, frac_coords, lattices, natoms: List[int], cond_scale: float = 2.0,
-                     step_lr: float = 1e-5, text_embeds=None, null_text_embeds=None, noise=None, seed: int = 0):
+                     step_lr: float = 1e-5, text_embeds=None, null_text_embeds=None, noise=None, seed: int = 0,
+                     node_base: int = 0, graph_base: int = 0):
         """One step t -> t-1 (chemeleon.py:379-466) from an explicit state.
         `noise` = (rand_a, rand_l, rand_x1, rand_x2) tensors or None (Philox).
         Returns new (atom_types, frac_coords, lattices) device tensors."""
@@ -327,7 +353,8 @@ class Chemeleon(nn.Module):
         _lib.require_device(a, x, lat, cond, null, *nz)
         _lib.check(_lib.load().chm_sample_step(batch.handle, sched, int(t), float(cond_scale), _lib.ptr(a),
                                                _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null),
-                                               *[_lib.ptr(z) for z in nz], seed, 0, 0, _lib.stream_handle(dev)),
+                                               *[_lib.ptr(z) for z in nz], seed, node_base, graph_base,
+                                               _lib.stream_handle(dev)),
                    "chm_sample_step")
         return a, x, lat
 
@@ -346,7 +373,10 @@ class Chemeleon(nn.Module):
     def sample(self, text_input: str, n_atoms: int, n_samples: int, cond_scale: float = 2.0, step_lr: float = 1e-5,
                return_trajectory: bool = False, stream: bool = False, **kw):
         """chemeleon.py:469-490. Without return_trajectory / stream, only the
-        final state is copied to the host (the reference converts every step)."""
+        final state is copied to the host (the reference converts every step).
+        Keyword arguments go to sample_states: noise="philox" (device noise,
+        one captured HIP graph replayed per timestep) or the default
+        noise="torch" (the reference's CPU RNG stream, eager launches)."""
         natoms = [n_atoms] * n_samples
         texts = [text_input] * n_samples if text_input is not None else None
         if stream:

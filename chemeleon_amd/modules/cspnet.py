@@ -8,7 +8,9 @@ runs in hand-written gfx950 kernels. There is no CPU fallback: calling
 forward with CPU tensors raises.
 """
 
+import ctypes
 import math
+import threading
 from collections import namedtuple
 from typing import Dict, Optional, Tuple
 
@@ -16,6 +18,8 @@ import torch
 import torch.nn as nn
 
 from chemeleon_amd import _lib
+
+_MATH_CODES = {"bf16x3": _lib.MATH_BF16X3, "f32": _lib.MATH_F32, "split16": _lib.MATH_SPLIT16}
 
 DECODER_OUTPUTS = namedtuple("DECODER_OUTPUTS", ["atom_types_out", "lattice_out", "coords_out", "node_features"])
 
@@ -97,15 +101,28 @@ class _HipModel:
 
 
 class HipBatch:
-    """Owns a chm_batch: index tables of the fc edge layout + workspace."""
+    """Owns a chm_batch: index tables of the fc edge layout + the decoder workspace.
+
+    The workspace is a uint8 tensor from the PyTorch caching allocator, allocated on the
+    stream that is current at creation (chm_batch_create_with_workspace), so its memory is
+    budgeted with the rest of the process's device tensors. A batch is scratch for one stream:
+    CSPNet.hip_batch keys its cache by stream."""
 
     def __init__(self, model: _HipModel, natoms, max_pairs: int):
         L = _lib.load()
         nat = [int(n) for n in natoms]
-        arr = (ctypes_int32 * len(nat))(*nat)
+        arr = (ctypes.c_int32 * len(nat))(*nat)
+        need = int(L.chm_batch_workspace_bytes(model.handle, arr, len(nat), max_pairs))
+        if need == 0:
+            _lib.check(-1, "chm_batch_workspace_bytes")
         h = _lib.c_void_p()
         with torch.cuda.device(model.device):
-            _lib.check(L.chm_batch_create(model.handle, arr, len(nat), max_pairs, h), "chm_batch_create")
+            # 256-byte alignment: the caching allocator returns 512-byte aligned blocks
+            self.workspace = torch.empty(need, dtype=torch.uint8, device=model.device)
+            _lib.check(L.chm_batch_create_with_workspace(model.handle, arr, len(nat), max_pairs,
+                                                         _lib.ptr(self.workspace), need,
+                                                         _lib.stream_handle(model.device), h),
+                       "chm_batch_create_with_workspace")
         self.handle = h
         self.model = model  # keep the weights alive
         self.natoms = tuple(nat)
@@ -121,11 +138,6 @@ class HipBatch:
                 _lib.load().chm_batch_destroy(self.handle)
         except Exception:
             pass
-
-
-import ctypes  # noqa: E402
-
-ctypes_int32 = ctypes.c_int32
 
 
 class CSPNet(nn.Module):
@@ -158,6 +170,8 @@ class CSPNet(nn.Module):
         self._hip: Optional[_HipModel] = None
         self._hip_sig = None
         self._batches: Dict[Tuple, HipBatch] = {}
+        self._math: Optional[str] = None  # set_math choice, re-applied when the packed weights are rebuilt
+        self._hip_lock = threading.RLock()
 
     # ------------------------------------------------------------------ HIP plumbing
     def chm_dims(self):
@@ -183,33 +197,50 @@ class CSPNet(nn.Module):
 
     def hip_model(self) -> _HipModel:
         self._check_supported()
-        sig = tuple((p.data_ptr(), p._version, str(p.device)) for p in self.parameters())
-        if self._hip is None or sig != self._hip_sig:
-            self._hip = _HipModel(self)
-            self._hip_sig = sig
-            self._batches.clear()
-        return self._hip
+        with self._hip_lock:
+            sig = tuple((p.data_ptr(), p._version, str(p.device)) for p in self.parameters())
+            if self._hip is None or sig != self._hip_sig:
+                self._hip = _HipModel(self)
+                self._hip_sig = sig
+                self._batches.clear()
+                if self._math is not None:
+                    _lib.check(_lib.load().chm_model_set_math(self._hip.handle, _MATH_CODES[self._math]),
+                               "chm_model_set_math")
+            return self._hip
 
     def set_math(self, mode: str):
-        """'split16' (default), 'bf16x3' or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h)."""
-        code = {"bf16x3": _lib.MATH_BF16X3, "f32": _lib.MATH_F32, "split16": _lib.MATH_SPLIT16}[mode]
-        m = self.hip_model()
-        _lib.check(_lib.load().chm_model_set_math(m.handle, code), "chm_model_set_math")
-        self._batches.clear()
+        """'split16' (default), 'bf16x3' or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h).
+        The choice survives rebuilds of the packed weights (load_state_dict, .to())."""
+        code = _MATH_CODES[mode]
+        with self._hip_lock:
+            m = self.hip_model()
+            _lib.check(_lib.load().chm_model_set_math(m.handle, code), "chm_model_set_math")
+            self._math = mode
+            self._batches.clear()
 
     def get_math(self) -> str:
         return {0: "bf16x3", 1: "f32", 2: "split16"}[_lib.load().chm_model_get_math(self.hip_model().handle)]
 
-    def hip_batch(self, natoms, max_pairs: int = 1) -> HipBatch:
-        key = (tuple(int(n) for n in natoms), max_pairs)
+    def hip_batch(self, natoms, max_pairs: int = 1, stream=None, private: bool = False) -> HipBatch:
+        """Workspace + edge tables for this crystal list, cached per (natoms, max_pairs, stream):
+        concurrent samplers on different streams never share scratch. private=True returns a
+        fresh, uncached batch (one per concurrent lane of a captured step)."""
         m = self.hip_model()
-        b = self._batches.get(key)
-        if b is None:
-            if len(self._batches) >= 4:
-                self._batches.pop(next(iter(self._batches)))
-            b = HipBatch(m, key[0], max_pairs)
-            self._batches[key] = b
-        return b
+        nat = tuple(int(n) for n in natoms)
+        if private:
+            return HipBatch(m, nat, max_pairs)
+        if stream is None:
+            stream = torch.cuda.current_stream(m.device)
+        key = (nat, max_pairs, int(stream.cuda_stream))
+        with self._hip_lock:
+            b = self._batches.get(key)
+            if b is None:
+                if len(self._batches) >= 4:
+                    self._batches.pop(next(iter(self._batches)))
+                with torch.cuda.stream(stream):
+                    b = HipBatch(m, nat, max_pairs)
+                self._batches[key] = b
+            return b
 
     # ------------------------------------------------------------------ forward
     def _run(self, pairs, atom_types, frac_coords, lattices, num_atoms, t, text, need_nodes=True):

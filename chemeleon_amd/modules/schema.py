@@ -140,3 +140,86 @@ def step_to_atoms(atom_types, frac_coords, lattices, num_atoms, idx: int = None)
         out.append(sort_atoms(make_atoms(a[off:off + n], lat[g], x[off:off + n])))
         off += n
     return out if idx is None else out[idx]
+
+
+# ---------------------------------------------------------------------------------------------
+# CIF output (the reference's scripts convert the sampled ase.Atoms with pymatgen's
+# AseAtomsAdaptor and write `gen_{i}.cif`, chemeleon/scripts/sample_prompt.py:38-42; neither
+# pymatgen nor ase is needed here): P1 cell + fractional coordinates + symbols.
+# ---------------------------------------------------------------------------------------------
+def cell_parameters(cell) -> tuple:
+    """(a, b, c, alpha, beta, gamma) in Angstrom / degrees of a row-vector cell [3, 3]."""
+    v = np.asarray(cell, dtype=np.float64).reshape(3, 3)
+    lens = np.linalg.norm(v, axis=1)
+
+    def ang(i, j):
+        d = lens[i] * lens[j]
+        return 90.0 if d == 0 else float(np.degrees(np.arccos(np.clip(np.dot(v[i], v[j]) / d, -1.0, 1.0))))
+
+    return float(lens[0]), float(lens[1]), float(lens[2]), ang(1, 2), ang(0, 2), ang(0, 1)
+
+
+def _formula_counts(symbols):
+    counts: Dict[str, int] = OrderedDict()
+    for s in symbols:
+        counts[s] = counts.get(s, 0) + 1
+    return counts
+
+
+def atoms_to_cif(atoms, name: Optional[str] = None) -> str:
+    """One structure (ase.Atoms or this module's Atoms) as a P1 CIF document."""
+    symbols = list(atoms.get_chemical_symbols())
+    frac = np.asarray(atoms.get_scaled_positions(), dtype=np.float64).reshape(-1, 3)
+    a, b, c, al, be, ga = cell_parameters(np.asarray(atoms.cell))
+    vol = float(abs(np.linalg.det(np.asarray(atoms.cell, dtype=np.float64).reshape(3, 3))))
+    counts = _formula_counts(sorted(symbols))
+    formula_sum = " ".join(f"{s}{n}" for s, n in counts.items())
+    name = name or "".join(f"{s}{n}" for s, n in counts.items())
+    lines = [
+        f"data_{name}",
+        "_symmetry_space_group_name_H-M   'P 1'",
+        f"_cell_length_a   {a:.8f}",
+        f"_cell_length_b   {b:.8f}",
+        f"_cell_length_c   {c:.8f}",
+        f"_cell_angle_alpha   {al:.8f}",
+        f"_cell_angle_beta   {be:.8f}",
+        f"_cell_angle_gamma   {ga:.8f}",
+        "_symmetry_Int_Tables_number   1",
+        f"_chemical_formula_structural   {name}",
+        f"_chemical_formula_sum   '{formula_sum}'",
+        f"_cell_volume   {vol:.8f}",
+        "_cell_formula_units_Z   1",
+        "loop_",
+        " _symmetry_equiv_pos_site_id",
+        " _symmetry_equiv_pos_as_xyz",
+        "  1  'x, y, z'",
+        "loop_",
+        " _atom_site_type_symbol",
+        " _atom_site_label",
+        " _atom_site_symmetry_multiplicity",
+        " _atom_site_fract_x",
+        " _atom_site_fract_y",
+        " _atom_site_fract_z",
+        " _atom_site_occupancy",
+    ]
+    seen: Dict[str, int] = {}
+    for s, (x, y, z) in zip(symbols, frac):
+        k = seen.get(s, 0)
+        seen[s] = k + 1
+        lines.append(f"  {s}  {s}{k}  1  {x:.8f}  {y:.8f}  {z:.8f}  1")
+    return "\n".join(lines) + "\n"
+
+
+def write_cif(atoms, path) -> str:
+    """Writes one structure to `path` (a .cif file); returns the path."""
+    path = str(path)
+    with open(path, "w") as f:
+        f.write(atoms_to_cif(atoms))
+    return path
+
+
+def save_structures(atoms_list, save_dir, prefix: str = "gen_") -> List[str]:
+    """The reference's output step (sample_prompt.py:38-42): `save_dir/gen_{i}.cif` per structure."""
+    import os
+    os.makedirs(str(save_dir), exist_ok=True)
+    return [write_cif(at, os.path.join(str(save_dir), f"{prefix}{i}.cif")) for i, at in enumerate(atoms_list)]

@@ -106,8 +106,20 @@ int chm_model_get_math(const chm_model* m);
  * calls) or 2 (cond + null classifier-free-guidance pairs). */
 int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs, chm_batch** out);
 void chm_batch_destroy(chm_batch* b);
-/* Device bytes the batch allocated (workspace + index tables). */
+/* Device bytes the batch uses (workspace + index tables). */
 size_t chm_batch_device_bytes(const chm_batch* b);
+
+/* Caller-owned workspace (SURVEY 8(b) Ownership): chm_batch_workspace_bytes returns the
+ * device bytes a batch of these crystals needs with the model's current arithmetic (0 on bad
+ * arguments), and chm_batch_create_with_workspace builds the batch inside the caller's
+ * allocation d_workspace (>= that many bytes, 256-byte aligned; e.g. a block from the PyTorch
+ * caching allocator). The index tables are uploaded on `stream`, which is synchronised before
+ * return; the workspace must outlive the batch, and chm_batch_destroy never frees it. A batch
+ * is scratch for one stream at a time: samplers that run concurrently on different streams use
+ * different batches. */
+size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs);
+int chm_batch_create_with_workspace(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs,
+                                    void* d_workspace, size_t workspace_bytes, void* stream, chm_batch** out);
 
 /* One decoder call for `pairs` conditionings that share atom types,
  * coordinates and lattices (pairs = 1: CSPNet.forward, cspnet.py:345-405;
@@ -175,6 +187,18 @@ int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, float* d_agg, 
 int chm_d3pm_sample(int N, int A, int T, const float* d_logits, const int64_t* d_xt, const int64_t* d_t,
                     const float* d_noise, const float* d_q_one_step, const float* d_q_mats, int64_t* d_out,
                     void* stream);
+
+/* Test hooks for the perf-mode noise (the device Philox4x32-10 streams the step kernels draw
+ * from; the reference draws torch.rand / torch.randn on its CPU generator instead,
+ * chemeleon.py:400-404,418,435,455):
+ *   chm_debug_philox: d_out[i] = uniform in [0,1) (normal = 0) or standard normal (normal = 1)
+ *     of key (seed, t, kind, base + i); kind 0 atom-type uniforms, 1 lattice, 2 / 3 coordinates.
+ *   chm_debug_d3pm_philox: chm_d3pm_sample with the Gumbel noise drawn from that stream (kind 0,
+ *     index (node_base + node) * 128 + class), as the sampler does in perf mode. */
+int chm_debug_philox(uint64_t seed, int t, int kind, int64_t base, int64_t n, int normal, float* d_out, void* stream);
+int chm_debug_d3pm_philox(int N, int A, int T, const float* d_logits, const int64_t* d_xt, const int64_t* d_t,
+                          const float* d_q_one_step, const float* d_q_mats, uint64_t seed, int64_t node_base,
+                          int64_t* d_out, void* stream);
 
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */

@@ -291,6 +291,43 @@ def gen_single_steps(chm, csp):
         save(f"step_{tag}.npz", **rec)
 
 
+def large_step_natoms(tag):
+    """Crystal sizes of the at-size single-step fixtures (BASELINE configs[2], the per-GPU
+    shard of configs[3], and a 256-crystal chunk of configs[4])."""
+    if tag == "256x40":
+        return [40] * 256
+    if tag == "64x40":
+        return [40] * 64
+    if tag == "c4chunk256":  # configs[4]: natoms = randint(1, 81, generator seed 7), first 256
+        return torch.randint(1, 81, (2048,), generator=torch.Generator().manual_seed(7))[:256].tolist()
+    raise KeyError(tag)
+
+
+LARGE_STEPS = (("256x40", [500]), ("64x40", [1000, 500, 1]), ("c4chunk256", [500]))
+
+
+def gen_large_steps(chm, csp):
+    """Teacher-forced single steps at BASELINE sizes (as gen_single_steps). Inputs and outputs
+    are stored; the noise is regenerated from its seed (torch CPU generator) by the test."""
+    T = 1000
+    m, sd = build_reference_model(chm, csp, T)
+    for tag, ts in LARGE_STEPS:
+        natoms = large_step_natoms(tag)
+        B, N = len(natoms), sum(natoms)
+        rec = {"natoms": torch.tensor(natoms), "ts": np.array(ts), "weights_crc": weights_crc(sd)}
+        for t in ts:
+            g = torch.Generator().manual_seed(2000 + t)
+            a = torch.randint(0, 104, (N,), generator=g)
+            a[::4] = 0
+            x = torch.rand(N, 3, generator=g)
+            lat = torch.randn(B, 3, 3, generator=g) * 3.0 * torch.tensor([[1, 0, 1], [1, 1, 1], [0, 0, 1]])
+            nxt = reference_single_step(m, natoms, a, x, lat, t, noise_seed=6000 + t)
+            rec[f"t{t}_a"], rec[f"t{t}_x"], rec[f"t{t}_l"] = a.to(torch.uint8), x, lat
+            rec[f"t{t}_a_out"] = nxt[0].to(torch.uint8)
+            rec[f"t{t}_x_out"], rec[f"t{t}_l_out"] = nxt[1], nxt[2]
+        save(f"step_{tag}.npz", **rec)
+
+
 def reference_single_step(m, natoms, a, x, lat, t, noise_seed):
     """Run the reference generator for exactly one step at time t from the
     given state. The loop iterator (`tqdm(range(T, 0, -1))`,
@@ -479,6 +516,8 @@ if __name__ == "__main__":
         gen_decoder(chm, csp)
     if "steps" in which:
         gen_single_steps(chm, csp)
+    if "steps_large" in which:
+        gen_large_steps(chm, csp)
     if "trajectory" in which:
         gen_trajectory(chm, csp)
     if "keys" in which:

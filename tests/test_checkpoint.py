@@ -65,3 +65,40 @@ def test_released_checkpoint_missing_is_explicit():
         pytest.skip("a released checkpoint is present")
     with pytest.raises(FileNotFoundError, match="figshare"):
         Chemeleon.load_general_text_model()
+
+
+def _tiny_text_encoder():
+    pytest.importorskip("transformers")
+    from chemeleon_amd.text_encoder import TextEncoder
+    bert = os.path.join(HERE, "golden", "tiny_bert")
+    torch.manual_seed(3)
+    return TextEncoder(text_encoder_name=bert, text_embed_dim=32, max_text_len=12, text_dim=24, local_path=bert)
+
+
+def test_checkpoint_text_encoder_weights_load_strictly(tmp_path):
+    """The trained conditioning head (text_emb.*, null_text_embeds) must come from the checkpoint;
+    only the frozen language model is sourced locally. A file without them is refused rather
+    than sampling with randomly initialised conditioning."""
+    m, cfg = _model()
+    te_src = _tiny_text_encoder()
+    with torch.no_grad():
+        for p in te_src.text_emb.parameters():
+            p.add_(1.0)
+        te_src.null_text_embeds.fill_(0.25)
+    sd = dict(m.state_dict())
+    for k, v in te_src.state_dict().items():
+        sd["text_encoder." + k] = v
+    path = tmp_path / "with-text.ckpt"
+    torch.save({"state_dict": sd, "hyper_parameters": dict(cfg)}, path)
+    m2 = Chemeleon.load_from_checkpoint(str(path), text_encoder=_tiny_text_encoder())
+    for k, v in te_src.state_dict().items():
+        if not k.startswith("text_encoder."):
+            assert torch.equal(m2.text_encoder.state_dict()[k], v), k
+    sd_bad = {k: v for k, v in sd.items() if not k.startswith("text_encoder.text_emb.")}
+    path2 = tmp_path / "without-head.ckpt"
+    torch.save({"state_dict": sd_bad, "hyper_parameters": dict(cfg)}, path2)
+    with pytest.raises(RuntimeError, match="text-encoder mismatch"):
+        Chemeleon.load_from_checkpoint(str(path2), text_encoder=_tiny_text_encoder())
+    m3 = Chemeleon.load_from_checkpoint(str(path2), text_encoder=_tiny_text_encoder(), strict=False)
+    assert m3.text_encoder is not None
+

@@ -25,6 +25,8 @@ def test_partition_balances_edge_work():
     assert max(work) / min(work) < 1.02
     assert [p[1] for p in parts[:-1]] == [p[0] for p in parts[1:]]
     assert partition([5, 5, 5], 3) == [(0, 1), (1, 2), (2, 3)]
+    with pytest.raises(ValueError, match="cannot be sharded"):
+        partition([5, 5], 3)
 
 
 def _free_port():
@@ -49,6 +51,17 @@ def _worker(rank, world, port, q):
         x = torch.arange(n0, n0 + N, dtype=torch.float32)[:, None].repeat(1, 3)
         lat = torch.arange(g0, g1, dtype=torch.float32)[:, None, None].repeat(1, 3, 3)
         A, X, LT, nat = gather_states((a, x, lat), local)
+        # with every rank's crystal list known up front: no size exchange, same result
+        A2, X2, LT2, nat2 = gather_states((a, x, lat), local, natoms_all=[nat_global[r0:r1] for r0, r1 in parts])
+        assert torch.equal(A, A2) and torch.equal(X, X2) and torch.equal(LT, LT2) and nat == nat2
+        # fewer crystals than ranks: every rank raises before any collective (no rank hangs)
+        from chemeleon_amd.distributed import sample_distributed
+        try:
+            sample_distributed(None, [4], cond=None, null=None)
+            raised = False
+        except ValueError:
+            raised = True
+        assert raised
         cond = torch.full((1, 4), float(rank == 0)) * 3.0
         null = torch.full((1, 4), float(rank == 0)) * 5.0
         c, n = broadcast_conditioning(cond, null)

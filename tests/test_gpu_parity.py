@@ -181,6 +181,65 @@ def test_teacher_forced_steps(model1000, golden, cn, tag, math):
         close(lat.cpu(), g[f"t{t}_l_out"], what=f"lattice t={t}")
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("tag", ["256x40", "64x40", "c4chunk256"])
+def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
+    """BASELINE sizes, one full reverse step each against the reference (fixtures written by the
+    reference itself, tests/golden/make_golden.py steps_large): configs[2] (256 x 40), the per-GPU
+    shard of configs[3] (64 x 40) and the first 256 crystals of configs[4]
+    (natoms = randint(1, 81, seed 7)), which puts crystals of 1 to 80 atoms, segment tiles that
+    span several small crystals and the gather path of the edge epilogues through the whole step.
+    Same gates as test_teacher_forced_steps: types bit-exact, |dx| <= 1e-4 periodic, lattices 1e-4."""
+    g = golden(f"step_{tag}.npz")
+    nat = g["natoms"].tolist()
+    B, N = len(nat), sum(nat)
+    if tag == "c4chunk256":
+        full = torch.randint(1, 81, (2048,), generator=torch.Generator().manual_seed(7)).tolist()
+        assert nat == full[:256] and min(nat) == 1 and max(nat) == 80
+    for t in g["ts"]:
+        t = int(t)
+        torch.manual_seed(6000 + t)
+        nz = None
+        if t > 1:
+            nz = (torch.rand((N, 104)), torch.randn(B, 3, 3), torch.randn(N, 3), torch.randn(N, 3))
+        a, x, lat = model1000.reverse_step(t, torch.from_numpy(g[f"t{t}_a"].astype(np.int64)),
+                                           torch.from_numpy(g[f"t{t}_x"]), torch.from_numpy(g[f"t{t}_l"]), nat,
+                                           2.0, 1e-5, cn[0], cn[1], noise=nz)
+        ref_a = g[f"t{t}_a_out"].astype(np.int64)
+        flips = int((a.cpu().numpy() != ref_a).sum())
+        assert flips == 0, f"{tag} t={t}: {flips} of {N} atom types differ"
+        dx = periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"{tag} frac t={t}")
+        dl = close(lat.cpu(), g[f"t{t}_l_out"], what=f"{tag} lattice t={t}")
+        print(f"{tag} t={t}: types bit-exact ({N} atoms), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
+
+
+@pytest.mark.timeout(300)
+def test_ragged_2048_full_size_step(model1000, cn):
+    """configs[4] at full size on one GPU (2048 crystals, natoms = randint(1, 81, seed 7),
+    Sum n^2 = 4.4 M edges per decoder call): one perf-mode step from pure noise and one at
+    t = 500 are finite and in range, and a crystal's result does not depend on the batch it
+    is sampled in (its slice of the 2048 batch equals the same crystals sampled alone)."""
+    nat = torch.randint(1, 81, (2048,), generator=torch.Generator().manual_seed(7)).tolist()
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(8)
+    a = torch.randint(0, 104, (N,), generator=g)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.randn(B, 3, 3, generator=g) * 3 * model1000.mask_lattice_matrix
+    for t in (1000, 500):
+        a2, x2, l2 = model1000.reverse_step(t, a, x, lat, nat, 2.0, 1e-5, cn[0], cn[1], noise=None, seed=3)
+        assert torch.isfinite(x2).all() and torch.isfinite(l2).all()
+        assert ((a2 >= 0) & (a2 < 104)).all()
+        assert ((x2 >= 0) & (x2 <= 1)).all()
+        if t == 1000:
+            assert (l2.abs() <= 6).all()
+    # the last 5 crystals alone (node_base / graph_base keep the Philox keys global)
+    g0 = B - 5
+    n0 = sum(nat[:g0])
+    sub = model1000.reverse_step(500, a[n0:], x[n0:], lat[g0:], nat[g0:], 2.0, 1e-5, cn[0], cn[1], noise=None,
+                                 seed=3, node_base=n0, graph_base=g0)
+    assert torch.equal(sub[0], a2[n0:]) and torch.equal(sub[1], x2[n0:]) and torch.equal(sub[2], l2[g0:])
+
+
 def _lattice_errors(lat, ref):
     """element-wise relative error (floored at 1e-3 of the state's largest entry)
     and normwise error (max abs error / max |entry|, per state)"""

@@ -1,5 +1,5 @@
 // Standalone microbenchmark of the decoder GEMM kernels (edge shapes at 512x40).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_bench.cpp chemeleon_amd/csrc/kernels.hip \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DCHM_MICROBENCH tools/gemm_bench.cpp chemeleon_amd/csrc/kernels.hip \
 //         chemeleon_amd/csrc/gemm_bf16x3.hip -o tools/gemm_bench && tools/gemm_bench
 #include <hip/hip_runtime.h>
 
@@ -83,15 +83,6 @@ int main(int argc, char** argv) {
     float t0 = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
     printf("M=%ld K=%d glds edge GEMM: %.3f ms %.1f TF fp32-eq; without C stores %.3f ms %.1f TF\n", M, K, te,
            flops / te / 1e9, t0, flops / t0 / 1e9);
-    {
-      EdgeArgs pa = ea;
-      float tp = time_it(5, s, [&] { CK(edge_gemm_pp(pa, EPI_STD, s)); });
-      pa.C = nullptr;
-      float tp0 = time_it(5, s, [&] { CK(edge_gemm_pp(pa, EPI_STD, s)); });
-      printf("  pp (2 WG/CU, 128x256): %.3f ms %.1f TF; without C stores %.3f ms %.1f TF\n", tp, flops / tp / 1e9, tp0,
-             flops / tp0 / 1e9);
-      if (getenv("PP_ONLY")) return 0;
-    }
     ea.C = nullptr;
     for (int rep = 0; rep < 3; ++rep)
       for (int var : {0, 3, 5, 7}) {
