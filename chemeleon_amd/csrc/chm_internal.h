@@ -75,6 +75,9 @@ struct EdgeArgs {
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
+// the same kernels on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)
+hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
+hipError_t edge16_init();
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);

@@ -1,0 +1,521 @@
+// The two split16 edge GEMMs of a CSP layer (cspnet.py:134-160: edge_mlp over all n^2 edges, then
+// scatter_mean) on v_mfma_f32_16x16x32_f16.
+//
+// Same operands, LDS rings, tiles and epilogue contracts as k_edge_gemm (edge_gemm.hip): split
+// rows [K/32][hi 32 | lo 32] fp16 staged by global_load_lds into a 3-deep A ring and a 2-deep W
+// ring, 256x256 output tiles, 8 waves of 64 rows x 128 columns, one block per CU, three fp16 MFMA
+// products per fp32 product. What differs is the MFMA shape. Both shapes run the matrix pipe at the
+// same FLOP per cycle, but under load the chip holds a higher clock on 16x16x32: back-to-back on
+// random operands at two waves per SIMD, 1.91 GHz against 1.67 GHz for 32x32x16 (+14% FLOP/s,
+// tools/mfma_shape_probe.hip, profiles/r2/mfma_shape_probe.log).
+//
+// Per K-tile of 32 a wave reads its four 16-row A fragments and, in four quarters of 32 columns,
+// its W fragments (lane l: row l & 15, k-chunk l >> 4 of the 128-B line, XOR-swizzled so every
+// 16-lane group of a ds_read_b128 covers all 64 banks); the 96 MFMAs of the tile run as four
+// quarters of 24 with the next quarter's fragment reads between them, the tile's barrier before
+// the last quarter, and the next tile's A fragments read under that quarter.
+//
+// Accumulators are C^T fragments: lane l holds edge row (l & 15) of each 16-row group and output
+// columns 16j + 4(l >> 4) .. +3 of each 16-column group j. Edge layer 1 stores S with the columns
+// of each 32-chunk permuted, 16a + 4g + r -> 8g + 4a + r (one 16-B store per plane), and W2's K
+// index is split with the same permutation (split_rows_h perm 2).
+#include "chm_internal.h"
+
+#include <type_traits>
+
+namespace chm {
+
+#include "edge_common.h"
+
+namespace {
+
+__device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// f(integral_constant<int, k>) for k = 0 .. N-1: compile-time register indices in epilogue loops
+// whose bodies are too large for the unroller (a runtime index would put acc in scratch)
+template <int K, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    static_for<K + 1, N>(f);
+  }
+}
+
+}  // namespace
+
+template <int EPI, bool ASC>
+__global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int ntn = g.N / BN;
+  const long bid = remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(bid % ntn) * BN;
+  long row0, nrows;
+  int seg_c = 0;
+  int2 seg = {0, 0};
+  if (EPI == EPI_SEGMEAN) {
+    const long rest = bid / ntn;
+    seg_c = (int)(rest % g.npairs);
+    seg = g.tiles[rest / g.npairs];
+    const long es0 = g.node_estart[seg.x];
+    const long es1 = (seg.y < g.nnodes) ? g.node_estart[seg.y] : g.E;
+    row0 = (long)seg_c * g.E + es0;
+    nrows = es1 - es0;
+  } else {
+    row0 = (bid / ntn) * BM;
+    nrows = g.M - row0 < BM ? g.M - row0 : BM;
+  }
+  const int K = g.K, nk = K / BK;
+
+  // ---- glds sources (as k_edge_gemm): wave w stages rows 32w..32w+31 of both operands, 8 rows per
+  // instruction; lane -> row 32w + 8q + (lane >> 3), LDS chunk lane & 7 holding line chunk
+  // (lane & 7) ^ swz(row), swz(row) = (row >> 1) & 7. A rows past nrows are read unclamped (F and S
+  // carry 256 rows of padding; those rows' results are never stored).
+  const char* Ab = reinterpret_cast<const char*>(g.A);
+  const char* Wb = reinterpret_cast<const char*>(g.W);
+  const long rowB = (long)K * 4;
+  const char* Ablk = Ab + row0 * rowB;
+  const char* Wblk = Wb + (long)n0 * rowB;
+  const int lr0 = wave * 32 + (lane >> 3);
+  const unsigned lc16 = 16u * (unsigned)((lane & 7) ^ ((lr0 >> 1) & 7));
+  const unsigned lc16x = lc16 ^ 64u;
+  const unsigned woff = (unsigned)(lr0 * rowB) + lc16;
+  const unsigned wq = (unsigned)(8 * rowB);
+  char* dst = lds + wave * 32 * ROW_B;
+  auto issueA = [&](int t) __attribute__((always_inline)) {
+    const char* src = Ablk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dst + (t % NSA) * OPND_B;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq + ((q & 1) ? (lc16x - lc16) : 0u))),
+                                       (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
+  };
+  auto issueW = [&](int t) __attribute__((always_inline)) {
+    const char* src = Wblk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dst + W_RING + (t % NSW) * OPND_B;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * wq + ((q & 1) ? (lc16x - lc16) : 0u))),
+                                       (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
+  };
+
+  // ---- row exponents of the A chunks (edge layer 2): the lane's four rows
+  int ex[4] = {0, 0, 0, 0};
+  if (ASC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long lr = wm * 64 + 16 * i + l16;
+      ex[i] = g.aexp[row0 + (lr < nrows ? lr : nrows - 1)];
+    }
+  }
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment of row r (16-row group base + l16), k-chunk g4 of plane p: logical chunk 4p + g4 at
+  // physical chunk (4p + g4) ^ swz(r); swz depends on l16 only (group bases are multiples of 16)
+  const int swz = (l16 >> 1) & 7;
+  const int ch0 = 16 * (g4 ^ swz), ch1 = 16 * ((4 + g4) ^ swz);
+  const int fa = (wm * 64 + l16) * ROW_B, fw = (wn * 128 + l16) * ROW_B;
+  f16x8 fA[2][2][4];  // [set][plane][row group]
+  f16x8 fW[2][2][2];  // [set][plane][column group of the quarter]
+  auto read_A = [&](int set, int t) __attribute__((always_inline)) {
+    const char* SA = lds + (t % NSA) * OPND_B + fa;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fA[set][0][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch0);
+      fA[set][1][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch1);
+    }
+  };
+  auto read_W = [&](int set, int t, int qq) __attribute__((always_inline)) {
+    const char* SW = lds + W_RING + (t % NSW) * OPND_B + fw + qq * 32 * ROW_B;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      fW[set][0][jj] = *reinterpret_cast<const f16x8*>(SW + jj * 16 * ROW_B + ch0);
+      fW[set][1][jj] = *reinterpret_cast<const f16x8*>(SW + jj * 16 * ROW_B + ch1);
+    }
+  };
+  // one quarter: columns 32qq .. 32qq+31 of the wave, all four row groups, three products
+  // (small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi)
+  auto mfq = [&](int aset, int wset, int qq) __attribute__((always_inline)) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][1][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][1][i], acc[i][2 * qq + jj]);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+  };
+  auto rescale = [&](int t) __attribute__((always_inline)) {
+    if (ASC && t > 0 && (t * BK) % CHUNK == 0) {
+      const int c = (t * BK) / CHUNK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ep = (int)(signed char)(ex[i] >> (8 * (c - 1)));
+        const int en = (int)(signed char)(ex[i] >> (8 * c));
+        const float f = ldexpf(1.0f, ep - en);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] *= f;
+      }
+    }
+  };
+  // quarter with n fragment reads spread between its 24 MFMAs (one per two MFMAs)
+  auto sched_reads = [&](auto NR) __attribute__((always_inline)) {
+    constexpr int nr = decltype(NR)::value;
+#pragma unroll
+    for (int k = 0; k < nr; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 24 - 2 * nr, 0);
+  };
+
+  // prologue (issue order W0 A0 A1 W1 A2, as k_edge_gemm): tile 0 landed when 12 glds remain
+  issueW(0);
+  issueA(0);
+  issueA(1);
+  issueW(1);
+  issueA(2);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_A(0, 0);
+  read_W(0, 0, 0);
+
+  // tile t: A fragments in set a = t & 1, W quarter fragments alternating sets 0, 1, 0, 1
+  auto tile = [&](int t, auto CUR) __attribute__((always_inline)) {
+    constexpr int a = decltype(CUR)::value;
+    rescale(t);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
+    __builtin_amdgcn_s_setprio(1);
+    read_W(1, t, 1);
+    mfq(a, 0, 0);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+    read_W(0, t, 2);
+    mfq(a, 1, 1);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+    read_W(1, t, 3);
+    mfq(a, 0, 2);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    // this wave is done reading tile t; this thread's part of tile t+1 has landed (only A(t+2) may
+    // still be in flight); after the barrier everyone's has, and tile t's stages are free
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    issueW(t + 2);  // past the end: re-reads of the last tile into idle stages
+    issueA(t + 3);
+    read_A(a ^ 1, t + 1);  // past the end: reads a re-read tile
+    read_W(0, t + 1, 0);
+    mfq(a, 1, 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  for (int t = 0; t < nk; t += 2) {  // nk = K / 32 is even (K = 512, 768)
+    tile(t, std::integral_constant<int, 0>{});
+    tile(t + 1, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the LDS is reused
+  __syncthreads();
+
+  // row scale of the last A chunk (edge layer 2)
+  float rs[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  if (ASC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
+  }
+  const int cw = n0 + wn * 128 + 4 * g4;  // this lane's first output column (+ 16 j)
+
+  if constexpr (EPI == EPI_STD) {
+    if (!g.C) return;  // (microbenchmark: main loop only)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long lr = wm * 64 + 16 * i + l16;
+        if (lr < nrows) *reinterpret_cast<f32x4*>(g.C + (row0 + lr) * g.ldc + cw + 16 * j) = acc[i][j] * sc * rs[i];
+      }
+    }
+    return;
+  }
+
+  if constexpr (EPI == EPI_EDGE) {
+    // S[c][e] = SiLU(D f + P_c[i] + Q_c[j]) as scaled hi/lo fp16 split rows (see k_edge_gemm's
+    // epilogue for the staging of the P / Q rows). First undo the W row scales.
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] *= sc;
+    }
+    const int PQ_ROWS = LDS_B / (PQ_PITCH * 4);
+    const long rl = row0 + nrows - 1;
+    const int ilo = g.ei[row0], ihi = g.ei[rl];
+    const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
+    const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
+    const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1, nR = nP + nQ;
+    const bool staged = nR <= PQ_ROWS;
+    const bool both = staged && g.npairs * nR <= PQ_ROWS;
+    const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
+    long rowv[4];
+    int pr[4], qr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long lr = wm * 64 + 16 * i + l16;
+      rowv[i] = row0 + (lr < nrows ? lr : nrows - 1);
+      pr[i] = g.ei[rowv[i]];
+      qr[i] = g.ej[rowv[i]];
+      if (staged) {
+        pr[i] -= ilo;
+        qr[i] = nP + qr[i] - jlo;
+      }
+    }
+    auto stage = [&](int c0, int c1) __attribute__((always_inline)) {  // conditionings [c0, c1), each at rows [rb, rb + nR)
+      if (c0 > 0) __syncthreads();     // everyone is done reading the previous conditioning
+      for (int c = c0; c < c1; ++c) {
+        const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+        const int rb = both ? c * nR : 0;
+        for (int r = wave; r < nR; r += 8) {
+          const float* src = Pc + (r < nP ? (long)(ilo + r) * (2 * H) : (long)(jlo + r - nP) * (2 * H) + H) + n0 + 4 * lane;
+          __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + PQ_OFF + (rb + r) * PQ_PITCH * 4), 16, 0,
+                                           0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
+    const bool nostore = g.dbg & 4;  // (profiling)
+    auto run = [&](int c, auto LAST, auto STG) __attribute__((always_inline)) {
+      constexpr bool last = decltype(LAST)::value, stg = decltype(STG)::value;
+      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+      const int rb = both ? c * nR : 0;
+      static_for<0, 4>([&](auto IC) __attribute__((always_inline)) {
+        constexpr int i = decltype(IC)::value;
+        const long lr = wm * 64 + 16 * i + l16;  // rows past nrows compute clamped copies, never stored
+        const float* prow;
+        const float* qrow;
+        if constexpr (stg) {
+          prow = T + (rb + pr[i]) * PQ_PITCH + wn * 128 + 4 * g4;
+          qrow = T + (rb + qr[i]) * PQ_PITCH + wn * 128 + 4 * g4;
+        } else {
+          prow = Pc + (long)pr[i] * (2 * H) + cw;
+          qrow = Pc + (long)qr[i] * (2 * H) + H + cw;
+        }
+        f32x4 v[8];  // SiLU values (the last conditioning's overwrite acc, which is no longer needed)
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 p = *reinterpret_cast<const f32x4*>(prow + 16 * j);
+          const f32x4 q = *reinterpret_cast<const f32x4*>(qrow + 16 * j);
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
+            const f32x2e x = silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]});
+            mx = fmaxf(mx, fmaxf(fabsf(x.x), fabsf(x.y)));
+            v[j][e] = x.x;
+            v[j][e + 1] = x.y;
+          }
+        }
+        // the row's 128 columns of this wave sit in the 4 lanes l16 + 16 g
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const int ex2 = exp_of(mx);
+        const float sc = ldexpf(1.0f, -ex2);
+        const long orow = (long)c * g.E + rowv[i];
+        _Float16* srow = S0 + orow * (2 * H) + ((n0 + wn * 128) / 32) * 64 + 8 * g4;
+        if (lr < nrows && !nostore) {
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {  // 32-column chunks: column groups 2cc, 2cc + 1
+            f16x8 hv, lv;
+#pragma unroll
+            for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float x = v[2 * cc + a2][r] * sc;
+                const _Float16 hx = (_Float16)x;
+                hv[4 * a2 + r] = hx;
+                lv[4 * a2 + r] = (_Float16)(x - (float)hx);
+              }
+            *reinterpret_cast<f16x8*>(srow + cc * 64) = hv;
+            *reinterpret_cast<f16x8*>(srow + cc * 64 + 32) = lv;
+          }
+          if (g4 == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+        }
+      });
+    };
+    using F = std::integral_constant<bool, false>;
+    using Tr = std::integral_constant<bool, true>;
+    auto all = [&](auto STG) __attribute__((always_inline)) {
+      constexpr bool stg = decltype(STG)::value;
+      if (g.npairs > 1) {
+        if (stg) stage(0, both ? 2 : 1);
+        run(0, F{}, STG);
+        if (stg && !both) stage(1, 2);
+        run(1, Tr{}, STG);
+      } else {
+        if (stg) stage(0, 1);
+        run(0, Tr{}, STG);
+      }
+    };
+    if (staged)
+      all(Tr{});
+    else
+      all(F{});
+    return;
+  }
+
+  if constexpr (EPI == EPI_SEGMEAN) {
+    // agg[c][node] = mean over the node's edges of SiLU(acc * wscale * rowscale + b2): the wn-th half
+    // of the waves writes its 128 columns to an LDS tile [256][132], then every thread sums node
+    // segments of one column in edge order (scatter_add's order) — as k_edge_gemm.
+    float* T = reinterpret_cast<float*>(lds);
+    int2* info = reinterpret_cast<int2*>(lds + SEG_B);
+    const int nn = seg.y - seg.x;
+    int2 my = {0, 0};
+    {
+      const long es0 = g.node_estart[seg.x];
+      if (tid < nn) {
+        const int nd = seg.x + tid;
+        my.x = g.node_n[nd];
+        my.y = (int)(g.node_estart[nd] - es0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // scale undo + bias + SiLU per column group; the next group's scale / bias loads are issued
+    // ahead of the current group's math (pinned there, else all 16 loads are hoisted and spill)
+    f32x4 scv[2], bbv[2];
+    scv[0] = *reinterpret_cast<const f32x4*>(g.wscale + cw);
+    bbv[0] = *reinterpret_cast<const f32x4*>(g.bias + cw);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < 7) {
+        scv[(j + 1) & 1] = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * (j + 1));
+        bbv[(j + 1) & 1] = *reinterpret_cast<const f32x4*>(g.bias + cw + 16 * (j + 1));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
+          const f32x2e s2 = f32x2e{scv[j & 1][e], scv[j & 1][e + 1]} * rs[i];
+          const f32x2e x = silu_e2(a2 * s2 + f32x2e{bbv[j & 1][e], bbv[j & 1][e + 1]});
+          acc[i][j][e] = x.x;
+          acc[i][j][e + 1] = x.y;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[i][j])::"memory");
+    }
+    for (int half = 0; half < 2; ++half) {
+      if (wn == half) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            *reinterpret_cast<f32x4*>(T + (wm * 64 + 16 * i + l16) * SEG_TP + 16 * j + 4 * g4) = acc[i][j];
+      }
+      if (half == 0 && tid < nn) info[tid] = my;
+      __syncthreads();
+      const int col = tid & 127;
+      for (int k = tid >> 7; k < nn; k += 4) {
+        const int2 ni = info[k];
+        const float* src = T + ni.y * SEG_TP + col;
+        float sacc = 0.f;
+        int jj = 0;
+        for (; jj + 8 <= ni.x; jj += 8) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = src[(jj + u) * SEG_TP];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sacc += v[u];
+        }
+        for (; jj < ni.x; ++jj) sacc += src[jj * SEG_TP];
+        const float mean = sacc / (float)(ni.x < 1 ? 1 : ni.x);
+        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = mean;
+        if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it (a wave = one node)
+          float m = fabsf(mean);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+          if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + seg.x + k, __float_as_uint(m));
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+hipError_t edge16_init() {
+  const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
+                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
+  if (g.N % BN || g.K % (2 * BK) || !g.A || !g.W || !g.wscale) return hipErrorInvalidValue;
+  const bool asc = g.aexp != nullptr;
+  if (asc && (g.K % CHUNK || g.K / CHUNK > 4)) return hipErrorInvalidValue;
+  long blocks;
+  if (epi == EPI_SEGMEAN) {
+    if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
+    blocks = (long)g.ntiles * g.npairs * (g.N / BN);
+  } else {
+    if (g.M <= 0) return hipErrorInvalidValue;
+    if (epi == EPI_EDGE &&
+        (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g || asc || g.npairs > 2))
+      return hipErrorInvalidValue;
+    blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
+  }
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = edge16_init();
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const dim3 grid((unsigned)blocks), block(512);
+  if (epi == EPI_EDGE)
+    hipLaunchKernelGGL((k_edge16<EPI_EDGE, false>), grid, block, LDS_B, s, g);
+  else if (epi == EPI_SEGMEAN)
+    hipLaunchKernelGGL((k_edge16<EPI_SEGMEAN, true>), grid, block, LDS_B, s, g);
+  else if (asc)
+    hipLaunchKernelGGL((k_edge16<EPI_STD, true>), grid, block, LDS_B, s, g);
+  else
+    hipLaunchKernelGGL((k_edge16<EPI_STD, false>), grid, block, LDS_B, s, g);
+  return hipGetLastError();
+}
+
+}  // namespace chm

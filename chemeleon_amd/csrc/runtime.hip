@@ -38,6 +38,7 @@ struct LayerW {
   const float *WAB, *Wcl, *b1, *D, *W2, *b2, *W3, *b3, *W4, *b4, *lw, *lb;
   const void *WAB3, *D3, *W23, *W33, *W43;  // bf16 hi/mid/lo planes of the GEMM weights
   void *D2h, *W22h;                          // fp16 hi/lo planes of the edge-GEMM weights (row-scaled)
+  void* W22h16;                              // W2's split rows with k_edge16's K permutation (perm 2)
   float *Dsc, *W2sc;                         // their per-row power-of-two scales
   void *WAB16, *W316, *W416;                 // split16 node GEMMs: fp16 hi/lo rows, 16-column chunks
   float *WABsc, *W3sc, *W4sc;                // (row-scaled like D2h)
@@ -62,6 +63,7 @@ struct chm_model {
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
+  int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
   std::vector<LayerW> layers;
@@ -118,6 +120,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   {
     hipError_t e0 = gemm_init();
     if (e0 == hipSuccess) e0 = edge_gemm_init();
+    if (e0 == hipSuccess) e0 = edge16_init();
     if (e0 == hipSuccess) e0 = node_gemm_init();
     if (e0 != hipSuccess) return fail(CHM_E_HIP, std::string("gemm_init: ") + hipGetErrorString(e0));
   }
@@ -230,6 +233,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
     if (tl) m->edge_trace_layer = atoi(tl);
+    const char* e16 = getenv("CHM_EDGE16");
+    if (e16) m->edge16 = atoi(e16);
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
     struct Job { const float* src; size_t n; const void** dst; };
@@ -264,17 +269,19 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       p3 += (3 * j.n * 2 + 255) / 256 * 256;
     }
     // fp16 hi/lo planes (+ row scales) of the two edge-GEMM weights of every layer
-    const size_t per_layer = (2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2 + 2 * H * 4 + 1023) / 1024 * 1024;
+    const size_t per_layer = (2 * (size_t)H * FD * 2 + 2 * 2 * (size_t)H * H * 2 + 2 * H * 4 + 1023) / 1024 * 1024;
     e2 = hipMalloc(&m->mem2, per_layer * L);
     for (int l = 0; l < L && e2 == hipSuccess; ++l) {
       char* q = (char*)m->mem2 + per_layer * l;
       LayerW& w = m->layers[l];
       w.D2h = q;
       w.W22h = q + 2 * (size_t)H * FD * 2;
-      w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2);
+      w.W22h16 = q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2;
+      w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * 2 * (size_t)H * H * 2);
       w.W2sc = w.Dsc + H;
       e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, 0, s);
       if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, 1, s);  // K permuted like S
+      if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h16, w.W2sc, 2, s);  // (k_edge16's S layout)
     }
     // fp16 hi/lo rows (16-column chunks, + row scales) of the node-GEMM weights (split16 node GEMMs)
     if (e2 == hipSuccess) {
@@ -723,19 +730,22 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
         HIPCHK(traced_edge_launch(m, ea, 1, E, s, [&] {
-          return edge_gemm(ea, EPI_EDGE, s);
+          return m->edge16 ? edge_gemm16(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s);
         }));
       }
       {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
         EdgeArgs ea;
         std::memset(&ea, 0, sizeof(ea));
         ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
-        ea.W = w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles; ea.ntiles = b->ntiles;
+        ea.W = m->edge16 ? w.W22h16 : w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles;
+        ea.ntiles = b->ntiles;
         ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
         ea.node_n = b->node_n; ea.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
         ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-        HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] { return edge_gemm(ea, EPI_SEGMEAN, s); }));
+        HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] {
+          return m->edge16 ? edge_gemm16(ea, EPI_SEGMEAN, s) : edge_gemm(ea, EPI_SEGMEAN, s);
+        }));
       }
     } else {
       {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
