@@ -183,7 +183,7 @@ def api_legs(model, n_samples, n_atoms, cond, null, seed, headline):
     return out
 
 
-def _pmc_traffic(math):
+def _pmc_traffic(math, kernel_key):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>/traffic.json;
     FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE). The counters cannot be
@@ -198,7 +198,7 @@ def _pmc_traffic(math):
             try:
                 ks = json.load(open(f))["kernels"]
                 for name, v in ks.items():
-                    if "k_edge_gemm<2" in name:
+                    if kernel_key in name:
                         return v["bytes_per_launch"], f"profiles/{rnd}/traffic.json ({name})"
             except Exception:  # noqa: BLE001
                 return None, None
@@ -318,7 +318,10 @@ def main():
     math = model.decoder.get_math()
     fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
-    traffic, traffic_src = _pmc_traffic(math) if not args.ragged else (None, "not collected for the ragged workload")
+    edge16 = os.environ.get("CHM_EDGE16", "1") != "0"
+    msg_kernel = "k_edge16<2" if edge16 else "k_edge_gemm<2"
+    traffic, traffic_src = (_pmc_traffic(math, msg_kernel) if not args.ragged else
+                            (None, "not collected for the ragged workload"))
     # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
     # = bf16 rate) / 3 products; f32 = the fp32 MFMA peak
     peak = {"bf16x3": BF16X3_PEAK_TFLOPS, "split16": MFMA_BF16_PEAK_TFLOPS / 3}.get(math, MFMA_F32_PEAK_TFLOPS)
@@ -371,8 +374,8 @@ def main():
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
-                     "kernel": {"split16": "edge message GEMM + fused scatter_mean (k_edge_gemm<EPI_SEGMEAN>), "
-                                           "both conditionings",
+                     "kernel": {"split16": f"edge message GEMM + fused scatter_mean ({msg_kernel}, EPI_SEGMEAN, "
+                                           f"{'16x16x32' if edge16 else '32x32x16'} MFMA), both conditionings",
                                 "bf16x3": "edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), "
                                           "both conditionings",
                                 "f32": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"}[math],
@@ -380,7 +383,8 @@ def main():
                      "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
-                                   "split16": "fp32-equivalent flops; fp16 dense MFMA 2.5 PF / 3 products",
+                                   "split16": "fp32-equivalent flops (3 fp16 MFMA products each); fp16 dense MFMA "
+                                           "2.5 PF / 3 products",
                                    "f32": "fp32 MFMA dense peak"}[math],
                      "flops_per_launch": msg_flops, "launches": nmsg,
                      "avg_ms": ms_msg / nmsg if nmsg else None},

@@ -70,8 +70,9 @@ struct EdgeArgs {
   unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
-  int dbg;  // profiling ablations (0 in the product): bit 0 = no K-loop loads, bit 1 = no barriers,
-            // bit 2 = no epilogue stores (EDGE / SEGMEAN), bit 3 = no PQ loads (EDGE)
+  int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
+            // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
+            // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN)
 };
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();

@@ -270,6 +270,14 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     return;
   }
 
+  if ((EPI == EPI_EDGE || EPI == EPI_SEGMEAN) && (g.dbg & 16)) {  // (profiling: main loop only)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+
   if constexpr (EPI == EPI_EDGE) {
     // S[c][e] = SiLU(D f + P_c[i] + Q_c[j]) as scaled hi/lo fp16 split rows (see k_edge_gemm's
     // epilogue for the staging of the P / Q rows). First undo the W row scales.
@@ -342,7 +350,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
-            const f32x2e x = silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]});
+            const f32x2e x = (g.dbg & 8) ? (a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]}  // (profiling)
+                                         : silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]});
             mx = fmaxf(mx, fmaxf(fabsf(x.x), fabsf(x.y)));
             v[j][e] = x.x;
             v[j][e + 1] = x.y;
@@ -430,7 +439,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
         for (int e = 0; e < 4; e += 2) {
           const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
           const f32x2e s2 = f32x2e{scv[j & 1][e], scv[j & 1][e + 1]} * rs[i];
-          const f32x2e x = silu_e2(a2 * s2 + f32x2e{bbv[j & 1][e], bbv[j & 1][e + 1]});
+          const f32x2e y = a2 * s2 + f32x2e{bbv[j & 1][e], bbv[j & 1][e + 1]};
+          const f32x2e x = (g.dbg & 8) ? y : silu_e2(y);  // (dbg 8: profiling)
           acc[i][j][e] = x.x;
           acc[i][j][e + 1] = x.y;
         }
@@ -448,7 +458,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
       if (half == 0 && tid < nn) info[tid] = my;
       __syncthreads();
       const int col = tid & 127;
-      for (int k = tid >> 7; k < nn; k += 4) {
+      for (int k = tid >> 7; k < nn && !(g.dbg & 32); k += 4) {  // (dbg 32: profiling, no sums)
         const int2 ni = info[k];
         const float* src = T + ni.y * SEG_TP + col;
         float sacc = 0.f;
