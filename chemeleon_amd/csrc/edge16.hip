@@ -194,7 +194,39 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
   read_A(0, 0);
   read_W(0, 0, 0);
 
-  // tile t: A fragments in set a = t & 1, W quarter fragments alternating sets 0, 1, 0, 1
+  // EPI_EDGE: the epilogue's P / Q rows are staged during the last K-tiles (their latency then hides
+  // under those MFMAs) when the ring layout allows it (nk % 6 == 0: tiles nk-3, nk-2 sit in A stages
+  // 0, 1 and tile nk-1 in A stage 2 / W stage 1) and the rows fit (nR <= PRE_MAX): conditioning 0 at
+  // row 0 (A stages 0-1, free after the barrier of tile nk-2), conditioning 1 at row PRE_ROW1 (free
+  // after the barrier of tile nk-1). Same scheme as k_edge_gemm.
+  bool pre = false;
+  int p_ilo = 0, p_jlo = 0, p_nP = 0, p_nR = 0;
+  if constexpr (EPI == EPI_EDGE) {
+    if (nk % 6 == 0 && !(g.dbg & 2048)) {
+      const long rl = row0 + nrows - 1;
+      // (block-uniform: kept in SGPRs, they stay live across the main loop)
+      p_ilo = __builtin_amdgcn_readfirstlane(g.ei[row0]);
+      const int ihi = __builtin_amdgcn_readfirstlane(g.ei[rl]);
+      const int ghi = __builtin_amdgcn_readfirstlane(g.n2g[ihi]);
+      p_jlo = __builtin_amdgcn_readfirstlane(g.node_off[__builtin_amdgcn_readfirstlane(g.n2g[p_ilo])]);
+      p_nP = ihi - p_ilo + 1;
+      p_nR = p_nP + __builtin_amdgcn_readfirstlane(g.node_off[ghi] + g.natoms[ghi]) - p_jlo;
+      pre = p_nR <= PRE_MAX;
+    }
+  }
+  auto stage_rows = [&](int c, int rbase) __attribute__((always_inline)) {
+    const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+    for (int r = wave; r < p_nR; r += 8) {
+      const float* src = Pc + (r < p_nP ? (long)(p_ilo + r) * (2 * H) : (long)(p_jlo + r - p_nP) * (2 * H) + H) + n0 +
+                         4 * lane;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(lds + (rbase + r) * PQ_PITCH * 4), 16, 0, 0);
+    }
+  };
+
+  // tile t: A fragments in set a = t & 1, W quarter fragments alternating sets 0, 1, 0, 1.
+  // Pre-staging blocks (EPI_EDGE) skip the loads past the end of K and stage conditioning 0's P / Q
+  // rows after the barrier of tile nk-2, conditioning 1's after that of nk-1 (block-uniform
+  // branches; the loop keeps its shape, which keeps the register allocation spill-free).
   auto tile = [&](int t, auto CUR) __attribute__((always_inline)) {
     constexpr int a = decltype(CUR)::value;
     rescale(t);
@@ -217,15 +249,25 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     sched_reads(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
     // this wave is done reading tile t; this thread's part of tile t+1 has landed (only A(t+2) may
-    // still be in flight); after the barrier everyone's has, and tile t's stages are free
+    // still be in flight; near the end everything is waited for); after the barrier everyone's
+    // has, and tile t's stages are free
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (t < nk - 2)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    issueW(t + 2);  // past the end: re-reads of the last tile into idle stages
-    issueA(t + 3);
-    read_A(a ^ 1, t + 1);  // past the end: reads a re-read tile
+    if (EPI == EPI_EDGE && pre && t >= nk - 3) {
+      if (t == nk - 3) issueW(t + 2);
+      if (t == nk - 2) stage_rows(0, 0);
+      if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
+    } else {
+      issueW(t + 2);  // past the end: re-reads of the last tile into idle stages
+      issueA(t + 3);
+    }
+    read_A(a ^ 1, t + 1);  // past the end: reads a re-read tile (or staged rows: never used)
     read_W(0, t + 1, 0);
     mfq(a, 1, 3);
 #pragma unroll
@@ -245,7 +287,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     tile(t, std::integral_constant<int, 0>{});
     tile(t + 1, std::integral_constant<int, 1>{});
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the LDS is reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads (or staged rows) land before the LDS is reused
   __syncthreads();
 
   // row scale of the last A chunk (edge layer 2)
@@ -293,8 +335,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
     const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
     const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1, nR = nP + nQ;
-    const bool staged = nR <= PQ_ROWS;
-    const bool both = staged && g.npairs * nR <= PQ_ROWS;
+    const bool staged = pre || nR <= PQ_ROWS;
+    const bool both = pre || (staged && g.npairs * nR <= PQ_ROWS);
     const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
     long rowv[4];
     int pr[4], qr[4];
@@ -310,6 +352,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
       }
     }
     auto stage = [&](int c0, int c1) __attribute__((always_inline)) {  // conditionings [c0, c1), each at rows [rb, rb + nR)
+      if (pre) return;                 // (staged by the main loop's last tiles)
       if (c0 > 0) __syncthreads();     // everyone is done reading the previous conditioning
       for (int c = c0; c < c1; ++c) {
         const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
@@ -328,7 +371,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     auto run = [&](int c, auto LAST, auto STG) __attribute__((always_inline)) {
       constexpr bool last = decltype(LAST)::value, stg = decltype(STG)::value;
       const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-      const int rb = both ? c * nR : 0;
+      const int rb = pre ? c * PRE_ROW1 : (both ? c * nR : 0);
       static_for<0, 4>([&](auto IC) __attribute__((always_inline)) {
         constexpr int i = decltype(IC)::value;
         const long lr = wm * 64 + 16 * i + l16;  // rows past nrows compute clamped copies, never stored
