@@ -499,7 +499,11 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
             *reinterpret_cast<f32x4*>(T + (wm * 64 + 16 * i + l16) * SEG_TP + 16 * j + 4 * g4) = acc[i][j];
       }
       if (half == 0 && tid < nn) info[tid] = my;
-      __syncthreads();
+      // LDS-only barriers in this loop: a __syncthreads() fence would also wait for the agg stores and
+      // the agg_max atomics still in flight (~3000 cycles each under load, twice per tile)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile rows and the node list are in LDS
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       const int col = tid & 127;
       for (int k = tid >> 7; k < nn && !(g.dbg & 32); k += 4) {  // (dbg 32: profiling, no sums)
         const int2 ni = info[k];
@@ -523,7 +527,9 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
           if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + seg.x + k, __float_as_uint(m));
         }
       }
-      __syncthreads();
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // everyone's tile reads are done before the next half is written
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
   }
 }
