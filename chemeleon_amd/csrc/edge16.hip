@@ -70,6 +70,17 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     nrows = g.M - row0 < BM ? g.M - row0 : BM;
   }
   const int K = g.K, nk = K / BK;
+  const unsigned long long t0 = g.trace ? rtime() : 0;  // (profiling: CHM_EDGE_TRACE block timelines)
+  unsigned long long tmain = 0;
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if (g.trace && tid == 0) g.trace[6 * blockIdx.x + slot] = rtime();
+  };
+  auto stamp_end = [&]() __attribute__((always_inline)) {
+    if (g.trace && tid == 0) {
+      unsigned long long* o = g.trace + 6 * blockIdx.x;
+      o[0] = hwid(); o[1] = t0; o[2] = tmain; o[3] = rtime();
+    }
+  };
 
   // ---- glds sources (as k_edge_gemm): wave w stages rows 32w..32w+31 of both operands, 8 rows per
   // instruction; lane -> row 32w + 8q + (lane >> 3), LDS chunk lane & 7 holding line chunk
@@ -259,15 +270,13 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if (EPI == EPI_EDGE && pre && t >= nk - 3) {
-      if (t == nk - 3) issueW(t + 2);
+    if (t + 2 < nk) issueW(t + 2);  // (nothing is loaded past the end of K)
+    if (t + 3 < nk) issueA(t + 3);
+    if (EPI == EPI_EDGE && pre) {
       if (t == nk - 2) stage_rows(0, 0);
       if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
-    } else {
-      issueW(t + 2);  // past the end: re-reads of the last tile into idle stages
-      issueA(t + 3);
     }
-    read_A(a ^ 1, t + 1);  // past the end: reads a re-read tile (or staged rows: never used)
+    read_A(a ^ 1, t + 1);  // past the end: reads stale stages (never used)
     read_W(0, t + 1, 0);
     mfq(a, 1, 3);
 #pragma unroll
@@ -287,8 +296,9 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
     tile(t, std::integral_constant<int, 0>{});
     tile(t + 1, std::integral_constant<int, 1>{});
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads (or staged rows) land before the LDS is reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (staged P / Q rows) land before the LDS is reused
   __syncthreads();
+  if (g.trace) tmain = rtime();
 
   // row scale of the last A chunk (edge layer 2)
   float rs[4] = {1.0f, 1.0f, 1.0f, 1.0f};
@@ -434,6 +444,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
       if (g.npairs > 1) {
         if (stg) stage(0, both ? 2 : 1);
         run(0, F{}, STG);
+        stamp(4);
         if (stg && !both) stage(1, 2);
         run(1, Tr{}, STG);
       } else {
@@ -445,6 +456,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
       all(Tr{});
     else
       all(F{});
+    stamp_end();
     return;
   }
 
@@ -490,7 +502,9 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
+    stamp(4);
     for (int half = 0; half < 2; ++half) {
+      if (half == 1) stamp(5);
       if (wn == half) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -531,6 +545,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+    stamp_end();
   }
 }
 

@@ -1,7 +1,8 @@
-# Block timelines of edge layer 1 (big and pp kernels, pp staggered). Repo root, GPU box.
-mkdir -p gpurun_out/trace
-for cfg in ${CFGS:-"0 0" "1 0" "1 8"}; do
-  set -- $(echo $cfg | tr _ " ")
-  CHM_EDGE_DBG=${DBG:-0} CHM_EDGE1_PP=$1 CHM_EDGE_STAGGER=${2:-0} CHM_EDGE_TRACE_LAYER=${LAYER:-1} CHM_EDGE_TRACE=gpurun_out/trace/t$1-$2.bin timeout -k 10 240 python bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline > gpurun_out/trace/b$1-$2.log 2>&1 || exit 1
-  echo "== pp $1 stagger $2"; python tools/trace_summary.py gpurun_out/trace/t$1-$2.bin ${SUMARGS:-}
+# Block timelines (CHM_EDGE_TRACE, s_memrealtime stamps) of edge layer 1 and 2 from one eager bench
+# pass; repo root, GPU box. Usage: tools/trace_run.sh <tag> [bench args]
+O=gpurun_out/${1:-trace}; shift
+mkdir -p $O
+for layer in 1 2; do
+  CHM_EDGE_TRACE_LAYER=$layer CHM_EDGE_TRACE=$O/t$layer.bin timeout -k 10 240 python bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-api-legs "$@" > $O/b$layer.log 2>&1 || exit 1
+  echo "== edge layer $layer"; python tools/trace_summary.py $O/t$layer.bin ${SUMARGS:-}
 done
