@@ -45,14 +45,15 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 }  // namespace
 
+// one output tile: virtual block vb of nvb (the XCD-aware remap turns it into a tile index)
 template <int EPI, bool ASC>
-__global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
+__device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int l16 = lane & 15, g4 = lane >> 4;
   const int ntn = g.N / BN;
-  const long bid = remap(blockIdx.x, gridDim.x);
+  const long bid = remap(vb, nvb);
   const int n0 = (int)(bid % ntn) * BN;
   long row0, nrows;
   int seg_c = 0;
@@ -73,11 +74,11 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
   const unsigned long long t0 = g.trace ? rtime() : 0;  // (profiling: CHM_EDGE_TRACE block timelines)
   unsigned long long tmain = 0;
   auto stamp = [&](int slot) __attribute__((always_inline)) {
-    if (g.trace && tid == 0) g.trace[6 * blockIdx.x + slot] = rtime();
+    if (g.trace && tid == 0) g.trace[6 * vb + slot] = rtime();
   };
   auto stamp_end = [&]() __attribute__((always_inline)) {
     if (g.trace && tid == 0) {
-      unsigned long long* o = g.trace + 6 * blockIdx.x;
+      unsigned long long* o = g.trace + 6 * vb;
       o[0] = hwid(); o[1] = t0; o[2] = tmain; o[3] = rtime();
     }
   };
@@ -549,9 +550,28 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
   }
 }
 
+// g.persist == 0: one tile per block. g.persist = T > 0: a persistent grid (about one block per CU)
+// walks the T tiles, and every other CU of each XCD starts g.stagger x 4 us late, so that half of
+// the CUs are in their main loop while the other half store their epilogue: edge layer 1's S
+// stores (512 KB per tile) then drain beside matrix work instead of in one chip-wide burst.
+template <int EPI, bool ASC, bool PERSIST = false>
+__global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
+  if constexpr (!PERSIST) {
+    edge16_tile<EPI, ASC>(g, blockIdx.x, gridDim.x);
+  } else {
+    if (g.stagger > 0 && ((blockIdx.x >> 3) & 1))
+      for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
+    for (long v = blockIdx.x; v < g.persist; v += gridDim.x) {
+      edge16_tile<EPI, ASC>(g, v, g.persist);
+      __syncthreads();  // the epilogue's LDS reads are done before the next tile's ring fills
+    }
+  }
+}
+
 hipError_t edge16_init() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
-                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>};
+                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
+                      (const void*)k_edge16<EPI_EDGE, false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
@@ -580,15 +600,23 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
+  EdgeArgs ga = g;
+  ga.persist = 0;
+  if (g.persist > 0 && blocks > 256) {  // (the caller asks for the persistent grid; g.persist = CUs)
+    ga.persist = blocks;
+    blocks = g.persist;
+  }
   const dim3 grid((unsigned)blocks), block(512);
-  if (epi == EPI_EDGE)
-    hipLaunchKernelGGL((k_edge16<EPI_EDGE, false>), grid, block, LDS_B, s, g);
+  if (epi == EPI_EDGE && ga.persist > 0)
+    hipLaunchKernelGGL((k_edge16<EPI_EDGE, false, true>), grid, block, LDS_B, s, ga);
+  else if (epi == EPI_EDGE)
+    hipLaunchKernelGGL((k_edge16<EPI_EDGE, false>), grid, block, LDS_B, s, ga);
   else if (epi == EPI_SEGMEAN)
-    hipLaunchKernelGGL((k_edge16<EPI_SEGMEAN, true>), grid, block, LDS_B, s, g);
+    hipLaunchKernelGGL((k_edge16<EPI_SEGMEAN, true>), grid, block, LDS_B, s, ga);
   else if (asc)
-    hipLaunchKernelGGL((k_edge16<EPI_STD, true>), grid, block, LDS_B, s, g);
+    hipLaunchKernelGGL((k_edge16<EPI_STD, true>), grid, block, LDS_B, s, ga);
   else
-    hipLaunchKernelGGL((k_edge16<EPI_STD, false>), grid, block, LDS_B, s, g);
+    hipLaunchKernelGGL((k_edge16<EPI_STD, false>), grid, block, LDS_B, s, ga);
   return hipGetLastError();
 }
 
