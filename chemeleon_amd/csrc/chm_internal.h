@@ -70,7 +70,6 @@ struct EdgeArgs {
   unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
-  long persist; // k_edge16: > 0 = persistent grid of that many blocks walking all tiles (0 = one tile per block)
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
             // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
             // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN)

@@ -417,25 +417,42 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         const int ex2 = exp_of(mx);
         const float sc = ldexpf(1.0f, -ex2);
         const long orow = (long)c * g.E + rowv[i];
-        _Float16* srow = S0 + orow * (2 * H) + ((n0 + wn * 128) / 32) * 64 + 8 * g4;
-        if (lr < nrows && !nostore) {
+        // Whole-line stores: a row's 32-column chunk is one 128-B line [hi 32 | lo 32], held by the
+        // row's four lanes (16 B of hi and 16 B of lo each). Lanes l16 and l16 ^ 1 (rows 2p, 2p+1)
+        // swap a piece (DPP), so that one store writes row 2p's whole line (even lanes its hi half,
+        // odd lanes its lo half) and the next row 2p+1's: 8 full lines per instruction instead of
+        // 16 half lines (the per-CU store path, not HBM, bounds this epilogue).
+        const bool odd = l16 & 1;
+        const long lre = lr & ~1L, lro = lr | 1L;  // the pair's rows (tile-relative)
+        const long orow_e = (long)c * g.E + row0 + lre, orow_o = orow_e + 1;
+        const int off = ((n0 + wn * 128) / 32) * 64 + 8 * g4 + (odd ? 32 : 0);
+        _Float16* se = S0 + orow_e * (2 * H) + off;
+        _Float16* so = S0 + orow_o * (2 * H) + off;
+        const bool st_e = lre < nrows && !nostore, st_o = lro < nrows && !nostore;
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {  // 32-column chunks: column groups 2cc, 2cc + 1
-            f16x8 hv, lv;
+        for (int cc = 0; cc < 4; ++cc) {  // 32-column chunks: column groups 2cc, 2cc + 1
+          f16x8 hv, lv;
 #pragma unroll
-            for (int a2 = 0; a2 < 2; ++a2)
+          for (int a2 = 0; a2 < 2; ++a2)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float x = v[2 * cc + a2][r] * sc;
-                const _Float16 hx = (_Float16)x;
-                hv[4 * a2 + r] = hx;
-                lv[4 * a2 + r] = (_Float16)(x - (float)hx);
-              }
-            *reinterpret_cast<f16x8*>(srow + cc * 64) = hv;
-            *reinterpret_cast<f16x8*>(srow + cc * 64 + 32) = lv;
-          }
-          if (g4 == 0) reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+            for (int r = 0; r < 4; ++r) {
+              const float x = v[2 * cc + a2][r] * sc;
+              const _Float16 hx = (_Float16)x;
+              hv[4 * a2 + r] = hx;
+              lv[4 * a2 + r] = (_Float16)(x - (float)hx);
+            }
+          // even lanes pass their lo piece to the odd partner, odd lanes their hi piece to the even
+          typedef int i32x4 __attribute__((ext_vector_type(4)));
+          const i32x4 snd = __builtin_bit_cast(i32x4, odd ? hv : lv);
+          i32x4 rcv;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) rcv[w] = __builtin_amdgcn_mov_dpp(snd[w], 0xB1, 0xF, 0xF, false);  // lane ^ 1
+          const f16x8 r8 = __builtin_bit_cast(f16x8, rcv);
+          if (st_e) *reinterpret_cast<f16x8*>(se + cc * 64) = odd ? r8 : hv;  // row 2p: hi (even), lo (odd)
+          if (st_o) *reinterpret_cast<f16x8*>(so + cc * 64) = odd ? lv : r8;  // row 2p+1
         }
+        if (lr < nrows && !nostore && g4 == 0)
+          reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
       });
     };
     using F = std::integral_constant<bool, false>;
@@ -550,28 +567,14 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   }
 }
 
-// g.persist == 0: one tile per block. g.persist = T > 0: a persistent grid (about one block per CU)
-// walks the T tiles, and every other CU of each XCD starts g.stagger x 4 us late, so that half of
-// the CUs are in their main loop while the other half store their epilogue: edge layer 1's S
-// stores (512 KB per tile) then drain beside matrix work instead of in one chip-wide burst.
-template <int EPI, bool ASC, bool PERSIST = false>
+template <int EPI, bool ASC>
 __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
-  if constexpr (!PERSIST) {
-    edge16_tile<EPI, ASC>(g, blockIdx.x, gridDim.x);
-  } else {
-    if (g.stagger > 0 && ((blockIdx.x >> 3) & 1))
-      for (int k = 0; k < g.stagger; ++k) __builtin_amdgcn_s_sleep(127);
-    for (long v = blockIdx.x; v < g.persist; v += gridDim.x) {
-      edge16_tile<EPI, ASC>(g, v, g.persist);
-      __syncthreads();  // the epilogue's LDS reads are done before the next tile's ring fills
-    }
-  }
+  edge16_tile<EPI, ASC>(g, blockIdx.x, gridDim.x);
 }
 
 hipError_t edge16_init() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
-                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
-                      (const void*)k_edge16<EPI_EDGE, false, true>};
+                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
@@ -600,16 +603,9 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  EdgeArgs ga = g;
-  ga.persist = 0;
-  if (g.persist > 0 && blocks > 256) {  // (the caller asks for the persistent grid; g.persist = CUs)
-    ga.persist = blocks;
-    blocks = g.persist;
-  }
+  const EdgeArgs& ga = g;
   const dim3 grid((unsigned)blocks), block(512);
-  if (epi == EPI_EDGE && ga.persist > 0)
-    hipLaunchKernelGGL((k_edge16<EPI_EDGE, false, true>), grid, block, LDS_B, s, ga);
-  else if (epi == EPI_EDGE)
+  if (epi == EPI_EDGE)
     hipLaunchKernelGGL((k_edge16<EPI_EDGE, false>), grid, block, LDS_B, s, ga);
   else if (epi == EPI_SEGMEAN)
     hipLaunchKernelGGL((k_edge16<EPI_SEGMEAN, true>), grid, block, LDS_B, s, ga);

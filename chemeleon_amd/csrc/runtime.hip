@@ -64,7 +64,6 @@ struct chm_model {
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
-  int edge_persist = 0;  // CHM_EDGE_PERSIST=n: edge layer 1 on a persistent grid of n blocks (k_edge16)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
   std::vector<LayerW> layers;
@@ -234,8 +233,6 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
     if (tl) m->edge_trace_layer = atoi(tl);
-    const char* ep = getenv("CHM_EDGE_PERSIST");
-    if (ep) m->edge_persist = atoi(ep);
     const char* e16 = getenv("CHM_EDGE16");
     if (e16) m->edge16 = atoi(e16);
     const char* stg = getenv("CHM_EDGE_STAGGER");
@@ -731,7 +728,6 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ea.ei = b->ei; ea.ej = b->ej; ea.PQ = b->PQ; ea.nnodes = N; ea.npairs = P; ea.E = E;
         ea.node_off = b->node_off; ea.natoms = b->natoms; ea.n2g = b->n2g;
         ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
-        ea.persist = m->edge16 ? m->edge_persist : 0;
         ProfScope ps(CHM_K_EDGE_FOURIER, s);
         HIPCHK(traced_edge_launch(m, ea, 1, E, s, [&] {
           return m->edge16 ? edge_gemm16(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s);
