@@ -66,6 +66,7 @@ SIGNATURES = {
     "chm_d3pm_sample": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     "chm_edge_features": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "chm_edge_features_split": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "chm_prof_enable": (c_int, [c_int]),
     "chm_prof_reset": (c_int, []),
     "chm_prof_read": (c_int, [c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),

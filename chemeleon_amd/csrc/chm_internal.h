@@ -48,7 +48,8 @@ enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 // [K/32][hi 32 | lo 32] (a 32-deep K-tile of a row = one 128-B line), three fp16 MFMA products,
 // staged by global_load_lds.
 struct EdgeArgs {
-  long M;
+  long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M) (k_edge16; k_edge_gemm: row_base 0)
+  long row_base;
   int N, K;
   const void* A;                  // split rows [rows][K/32][2][32] fp16, readable 256 rows past the last
   const int* aexp;               // per A row: 4 packed int8 exponents of its 128-column chunks, or null
@@ -78,6 +79,9 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
 // the same kernels on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)
 hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
+// one grid: edge layer 1 (EPI_EDGE, g1: a row range) first, then edge layer 2 (EPI_SEGMEAN, g2: segment
+// tiles that read none of g1's rows)
+hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s);
 hipError_t edge16_init();
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
@@ -96,6 +100,7 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s);
 hipError_t node_gemm_init();
 extern int g_node_variant;  // microbenchmark probes of node_gemm (0 in the product)
 extern int g_node_blocks;   // S16 node GEMM blocks per CU override (microbenchmarks; 0 = default)
+extern int g_node_ks;       // S16 node GEMM K-interleave: 1 or 2 wave groups per tile
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)

@@ -67,7 +67,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     row0 = (long)seg_c * g.E + es0;
     nrows = es1 - es0;
   } else {
-    row0 = (bid / ntn) * BM;
+    row0 = g.row_base + (bid / ntn) * BM;
     nrows = g.M - row0 < BM ? g.M - row0 : BM;
   }
   const int K = g.K, nk = K / BK;
@@ -572,14 +572,48 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
   edge16_tile<EPI, ASC>(g, blockIdx.x, gridDim.x);
 }
 
+// Edge layer 1's partial last round and edge layer 2 in one grid: blocks [0, nb1) are layer-1 tiles
+// (g1, rows [g1.row_base, g1.M)), the rest layer-2 segment tiles (g2) that read none of those rows.
+// Workgroups are dispatched in index order, so the layer-1 tiles start first and the layer-2 tiles fill
+// the CUs they leave idle; nb1 is a multiple of 8 (blocks past the layer-1 tiles return at once), so
+// the layer-2 part keeps its XCD-aware tile order.
+__global__ __launch_bounds__(512, 1) void k_edge16_tail(EdgeArgs g1, EdgeArgs g2, int nb1, int nt1) {
+  if ((int)blockIdx.x < nb1) {
+    if ((int)blockIdx.x < nt1) edge16_tile<EPI_EDGE, false>(g1, blockIdx.x, nt1);
+  } else {
+    edge16_tile<EPI_SEGMEAN, true>(g2, blockIdx.x - nb1, gridDim.x - nb1);
+  }
+}
+
 hipError_t edge16_init() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
-                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>};
+                      (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
+                      (const void*)k_edge16_tail};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s) {
+  if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
+      !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.M <= g1.row_base || g1.row_base < 0)
+    return hipErrorInvalidValue;
+  if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.tiles || g2.ntiles < 1 || !g2.agg || !g2.bias ||
+      !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = edge16_init();
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long nt1 = ((g1.M - g1.row_base + BM - 1) / BM) * (g1.N / BN);
+  const long nb1 = (nt1 + 7) / 8 * 8;
+  const long nt2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
+  hipLaunchKernelGGL(k_edge16_tail, dim3((unsigned)(nb1 + nt2)), dim3(512), LDS_B, s, g1, g2, (int)nb1, (int)nt1);
+  return hipGetLastError();
 }
 
 hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
@@ -591,11 +625,11 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
     if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
     blocks = (long)g.ntiles * g.npairs * (g.N / BN);
   } else {
-    if (g.M <= 0) return hipErrorInvalidValue;
+    if (g.M <= g.row_base || g.row_base < 0) return hipErrorInvalidValue;
     if (epi == EPI_EDGE &&
         (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g || asc || g.npairs > 2))
       return hipErrorInvalidValue;
-    blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
+    blocks = ((g.M - g.row_base + BM - 1) / BM) * (g.N / BN);
   }
   static bool attr = false;
   if (!attr) {

@@ -742,7 +742,7 @@ hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s) {
     if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
     blocks = (long)g.ntiles * g.npairs * (g.N / BN);
   } else {
-    if (g.M <= 0) return hipErrorInvalidValue;
+    if (g.M <= 0 || g.row_base) return hipErrorInvalidValue;  // (row ranges: k_edge16 only)
     if (epi == EPI_EDGE && (g.N != H || !g.S || !g.sexp || !g.PQ || !g.node_off || !g.natoms || !g.n2g || asc)) return hipErrorInvalidValue;
     blocks = ((g.M + BM - 1) / BM) * (g.N / BN);
   }

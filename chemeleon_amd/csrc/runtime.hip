@@ -64,6 +64,8 @@ struct chm_model {
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
+  int edge_split = 0;    // CHM_EDGE_SPLIT=1: partial-round tail split of edge layer 1 (see run_decoder)
+  int ncu = 0;           // compute units of the device the model lives on
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
   std::vector<LayerW> layers;
@@ -87,6 +89,11 @@ struct chm_batch {
   unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
   void* owned = nullptr;  // the library's own allocation (chm_batch_create); null for caller workspaces
   size_t bytes = 0;
+  // edge layer 1's partial last round (split16 / k_edge16, see run_decoder): rows [0, l1_rows_a) fill
+  // whole rounds of the grid; the rest runs in one grid with the segment tiles before l2_tile_a (which
+  // read none of those rows), the segment tiles from l2_tile_a on after it. 0 = no split.
+  long l1_rows_a = 0;
+  int l2_tile_a = 0;
 };
 
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
@@ -237,6 +244,13 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (e16) m->edge16 = atoi(e16);
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
+    const char* nks = getenv("CHM_NODE_KS");
+    if (nks) g_node_ks = atoi(nks) == 2 ? 2 : 1;
+    const char* spl = getenv("CHM_EDGE_SPLIT");
+    if (spl) m->edge_split = atoi(spl);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      m->ncu = 0;
     struct Job { const float* src; size_t n; const void** dst; };
     std::vector<Job> jobs;
     jobs.push_back({m->Wc, (size_t)2 * H * CIN, &m->Wc3});
@@ -494,6 +508,20 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     return fail(CHM_E_ARG, "workspace too small or not 256-byte aligned (need " + std::to_string(need) + " bytes)");
   }
   b->bytes = batch_layout(b, m, base, b->ntiles);
+  {  // edge layer 1 tail split: whole rounds of 256x256 tiles first (needs ncu, an even count of tiles)
+    const long tiles1 = (t.E + kTileRows - 1) / kTileRows * (H / 256);
+    if (m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu) {
+      long full = tiles1 / m->ncu * m->ncu;
+      full -= full % (H / 256);
+      const long rows_a = full / (H / 256) * kTileRows;
+      int ta = 0;
+      while (ta < (int)t.tiles.size() && (t.tiles[ta].y < t.N ? t.estart[t.tiles[ta].y] : t.E) <= rows_a) ++ta;
+      if (rows_a < t.E && ta > 0 && ta < (int)t.tiles.size()) {
+        b->l1_rows_a = rows_a;
+        b->l2_tile_a = ta;
+      }
+    }
+  }
   // index tables (setup only: the host vectors must outlive the copies, so the stream is drained)
   hipError_t e = hipSuccess;
   auto up = [&](void* dst, const void* src, size_t bytes) {
@@ -721,30 +749,46 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // split16: fp16 hi/lo split rows throughout (edge_gemm.hip). S lives in S's bytes as
       // split rows [P*E][H/32][2][32] plus one packed exponent word per row (rowmax buffer).
       int* sexp = reinterpret_cast<int*>(b->rowmax);
-      {  // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
-        EdgeArgs ea;
-        std::memset(&ea, 0, sizeof(ea));
-        ea.M = E; ea.N = H; ea.K = FD; ea.A = b->F; ea.W = w.D2h; ea.wscale = w.Dsc;
-        ea.ei = b->ei; ea.ej = b->ej; ea.PQ = b->PQ; ea.nnodes = N; ea.npairs = P; ea.E = E;
-        ea.node_off = b->node_off; ea.natoms = b->natoms; ea.n2g = b->n2g;
-        ea.S = b->S; ea.sexp = sexp; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
-        ProfScope ps(CHM_K_EDGE_FOURIER, s);
-        HIPCHK(traced_edge_launch(m, ea, 1, E, s, [&] {
-          return m->edge16 ? edge_gemm16(ea, EPI_EDGE, s) : edge_gemm(ea, EPI_EDGE, s);
-        }));
-      }
-      {  // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
-        EdgeArgs ea;
-        std::memset(&ea, 0, sizeof(ea));
-        ea.M = (long)P * E; ea.N = H; ea.K = H; ea.A = b->S; ea.aexp = sexp;
-        ea.W = m->edge16 ? w.W22h16 : w.W22h; ea.wscale = w.W2sc; ea.bias = w.b2; ea.tiles = b->tiles;
-        ea.ntiles = b->ntiles;
-        ea.node_estart = b->node_estart; ea.natoms = b->natoms; ea.n2g = b->n2g; ea.agg = b->agg;
-        ea.node_n = b->node_n; ea.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
-        ea.nnodes = N; ea.npairs = P; ea.E = E; ea.dbg = m->edge_dbg; ea.stagger = m->edge_stagger;
+      // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
+      EdgeArgs e1;
+      std::memset(&e1, 0, sizeof(e1));
+      e1.M = E; e1.N = H; e1.K = FD; e1.A = b->F; e1.W = w.D2h; e1.wscale = w.Dsc;
+      e1.ei = b->ei; e1.ej = b->ej; e1.PQ = b->PQ; e1.nnodes = N; e1.npairs = P; e1.E = E;
+      e1.node_off = b->node_off; e1.natoms = b->natoms; e1.n2g = b->n2g;
+      e1.S = b->S; e1.sexp = sexp; e1.dbg = m->edge_dbg; e1.stagger = m->edge_stagger;
+      // edge layer 2 fused with the aggregation: agg = mean_j SiLU(S W2^T + b2)
+      EdgeArgs e2;
+      std::memset(&e2, 0, sizeof(e2));
+      e2.M = (long)P * E; e2.N = H; e2.K = H; e2.A = b->S; e2.aexp = sexp;
+      e2.W = m->edge16 ? w.W22h16 : w.W22h; e2.wscale = w.W2sc; e2.bias = w.b2; e2.tiles = b->tiles;
+      e2.ntiles = b->ntiles;
+      e2.node_estart = b->node_estart; e2.natoms = b->natoms; e2.n2g = b->n2g; e2.agg = b->agg;
+      e2.node_n = b->node_n; e2.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
+      e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
+      if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !g_prof_on && !m->edge_trace) {
+        // Edge layer 1 in whole rounds of the grid (rows [0, l1_rows_a)), then one grid with its
+        // partial last round first and edge layer 2's segment tiles that do not read those rows
+        // behind it, then the segment tiles that do. Same tiles, same arithmetic: bit-identical to
+        // one launch per layer.
+        EdgeArgs e1b = e1, e2b = e2;
+        e1.M = b->l1_rows_a;
+        e1b.row_base = b->l1_rows_a;
+        e2.ntiles = b->l2_tile_a;
+        e2b.tiles = b->tiles + b->l2_tile_a;
+        e2b.ntiles = b->ntiles - b->l2_tile_a;
+        HIPCHK(edge_gemm16(e1, EPI_EDGE, s));
+        HIPCHK(edge_gemm16_tail(e1b, e2, s));
+        HIPCHK(edge_gemm16(e2b, EPI_SEGMEAN, s));
+      } else {
+        {
+          ProfScope ps(CHM_K_EDGE_FOURIER, s);
+          HIPCHK(traced_edge_launch(m, e1, 1, E, s, [&] {
+            return m->edge16 ? edge_gemm16(e1, EPI_EDGE, s) : edge_gemm(e1, EPI_EDGE, s);
+          }));
+        }
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-        HIPCHK(traced_edge_launch(m, ea, 2, E, s, [&] {
-          return m->edge16 ? edge_gemm16(ea, EPI_SEGMEAN, s) : edge_gemm(ea, EPI_SEGMEAN, s);
+        HIPCHK(traced_edge_launch(m, e2, 2, E, s, [&] {
+          return m->edge16 ? edge_gemm16(e2, EPI_SEGMEAN, s) : edge_gemm(e2, EPI_SEGMEAN, s);
         }));
       }
     } else {
@@ -901,5 +945,11 @@ extern "C" int chm_debug_d3pm_philox(int N, int A, int T, const float* logits, c
 extern "C" int chm_edge_features(chm_batch* b, const float* x, float* feat, void* stream) {
   if (!b || !x || !feat) return fail(CHM_E_ARG, "NULL argument");
   HIPCHK(fourier(x, b->ei, b->ej, b->E, feat, (hipStream_t)stream));
+  return CHM_OK;
+}
+
+extern "C" int chm_edge_features_split(chm_batch* b, const float* x, void* split, void* stream) {
+  if (!b || !x || !split) return fail(CHM_E_ARG, "NULL argument");
+  HIPCHK(fourier_h(x, b->ei, b->ej, b->E, split, (hipStream_t)stream));
   return CHM_OK;
 }

@@ -203,6 +203,10 @@ int chm_debug_d3pm_philox(int N, int A, int T, const float* d_logits, const int6
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */
 int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* stream);
+/* The same features in the form the split16 edge GEMM consumes (the sampler's k_fourier_h):
+ * d_split [E, 6*num_freqs/32, 2, 32] fp16, per 32-column chunk the hi parts then the lo parts
+ * (feature = hi + lo, |lo| <= 2^-11 |hi|); E * 6*num_freqs * 4 bytes. */
+int chm_edge_features_split(chm_batch* b, const float* d_frac, void* d_split, void* stream);
 
 /* Bench instrumentation: while enabled, the runtime brackets every launch of
  * the kernels below with HIP events on the launch stream (a pool of 8192

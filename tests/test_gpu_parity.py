@@ -97,6 +97,29 @@ def test_fourier_features(model1000, golden):
     np.testing.assert_allclose(feat.cpu().numpy(), ref.numpy(), atol=2e-6, rtol=0)
 
 
+def test_fourier_features_split(model1000, golden):
+    """The sampler's split16 Fourier kernel (k_fourier_h): hi + lo reproduces the oracle features
+    (cspnet.py:38-52) to fp32 rounding, hi is the fp16 rounding of the feature, and the lo part
+    carries the rest (|lo| <= ulp_fp16(hi) / 2)."""
+    g = golden("decoder_ragged.npz")
+    nat = g["natoms"].tolist()
+    x = torch.from_numpy(g["frac"])
+    b = model1000.decoder.hip_batch(nat, 1)
+    E = b.num_edges
+    raw = torch.empty(E, 768 * 2, dtype=torch.float16, device=DEV)
+    xd = x.to(DEV)
+    _lib.check(_lib.load().chm_edge_features_split(b.handle, _lib.ptr(xd), _lib.ptr(raw), _lib.stream_handle()), "fs")
+    r = raw.view(E, 24, 2, 32).cpu()
+    hi, lo = r[:, :, 0, :].reshape(E, 768), r[:, :, 1, :].reshape(E, 768)
+    e = O.fc_edges(nat)
+    ref = O.fourier((x[e[1]] - x[e[0]]) % 1.0, 128)
+    np.testing.assert_allclose((hi.float() + lo.float()).numpy(), ref.numpy(), atol=2e-6, rtol=0)
+    # hi is the fp16 rounding of the kernel's own fp32 feature, so it can differ from fp16(ref) only
+    # where ref sits within fp32 rounding of an fp16 rounding boundary
+    assert (hi != ref.half()).float().mean().item() < 1e-3
+    assert (lo.float().abs() <= hi.float().abs() * 2.0 ** -11 + 2.0 ** -25).all()
+
+
 def test_segment_mean_matches_oracle(model1000):
     nat = [3, 7, 1, 12, 40]
     b = model1000.decoder.hip_batch(nat, 2)
@@ -211,6 +234,33 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
         dx = periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"{tag} frac t={t}")
         dl = close(lat.cpu(), g[f"t{t}_l_out"], what=f"{tag} lattice t={t}")
         print(f"{tag} t={t}: types bit-exact ({N} atoms), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
+
+
+@pytest.mark.parametrize("nat", [[40] * 64, [40] * 256, [23, 7, 40, 1, 80] * 30])
+def test_edge_tail_split_is_bit_identical(model1000, cn, nat):
+    """When edge layer 1's 256x256 tiles do not fill whole rounds of the grid (64 x 40: 800 tiles on
+    256 CUs), the runtime runs the partial round on a forked stream beside edge layer 2 (runtime.hip,
+    run_decoder). Instrumented launches (chm_prof_enable) take the single-launch path, so the two
+    paths can be compared: one reverse step must agree bit for bit."""
+    lib = _lib.load()
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(11)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    outs = []
+    for prof in (0, 1):
+        _lib.check(lib.chm_prof_enable(prof), "prof")
+        try:
+            outs.append([o.cpu() for o in model1000.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1],
+                                                                  noise=nz)])
+        finally:
+            _lib.check(lib.chm_prof_enable(0), "prof")
+            _lib.check(lib.chm_prof_reset(), "prof")
+    for u, v, what in zip(outs[0], outs[1], ("types", "frac", "lattice")):
+        assert torch.equal(u, v), f"{what}: split and single-launch edge layers differ"
 
 
 @pytest.mark.timeout(300)

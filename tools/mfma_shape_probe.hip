@@ -86,7 +86,8 @@ void run(const _Float16* src, float* out, unsigned long long* clk, int blocks, i
   double cs = 0, rs = 0;
   for (int b = 0; b < blocks; ++b) { cs += h[2 * b]; rs += h[2 * b + 1]; }
   const double ghz = cs / rs * 0.1;  // s_memrealtime ticks at 100 MHz
-  const double flops = (double)blocks * 4 * WPS * iters * 3.0 * 8 * (32.0 * 32 * 16 * 2);  // same per shape
+  // per iteration: 3 x 8 MFMAs of 32x32x16 or 3 x 32 MFMAs of 16x16x32 (twice the flops of the former)
+  const double flops = (double)blocks * 4 * WPS * iters * 3.0 * (SHAPE == 32 ? 8 * 32768.0 : 32 * 16384.0);
   printf("%-28s %8.3f ms %7.1f TF  clock %.2f GHz\n", name, ms, flops / ms / 1e9, ghz);
 }
 
