@@ -42,6 +42,7 @@ SIGNATURES = {
     "chm_model_create": (c_int, [ctypes.POINTER(chm_dims), ctypes.POINTER(c_void_p), c_int, c_void_p,
                                  ctypes.POINTER(c_void_p)]),
     "chm_model_destroy": (None, [c_void_p]),
+    "chm_model_set_option": (c_int, [c_void_p, ctypes.c_char_p, c_i64]),
     "chm_model_set_math": (c_int, [c_void_p, c_int]),
     "chm_model_get_math": (c_int, [c_void_p]),
     "chm_batch_create": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, ctypes.POINTER(c_void_p)]),

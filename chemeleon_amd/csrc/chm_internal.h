@@ -69,6 +69,11 @@ struct EdgeArgs {
   const int* node_n;             // EPI_SEGMEAN: atom count of each node's crystal
   float* agg;
   unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
+  // k_edge16_tail: per layer-1 row tile from flag_row0 on, the count of its finished column tiles
+  // (EPI_EDGE bumps, EPI_SEGMEAN tiles reading rows >= flag_row0 wait); null = no intra-grid waits.
+  // zero_flags / nzero: an EPI_EDGE launch's block 0 clears them for the next grid.
+  unsigned* flags; long flag_row0;
+  unsigned* zero_flags; int nzero;
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no

@@ -115,6 +115,29 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
                                        (lds_void*)(d + q * 8 * ROW_B), 16, 0, 0);
   };
 
+  if (EPI == EPI_EDGE && g.zero_flags && vb == 0 && tid < g.nzero) g.zero_flags[tid] = 0u;  // (for the next grid)
+  if (EPI == EPI_SEGMEAN && g.flags) {
+    // k_edge16_tail: a segment tile whose edge rows reach into [flag_row0, E) waits until the layer-1
+    // tiles of this grid that write those rows (dispatched first, never waiting themselves) have
+    // published them, then acquires at agent scope before any load of S or its exponents. The spin
+    // is bounded (~0.3 s), so a broken invariant can never hang the device.
+    const long e0 = row0 - (long)seg_c * g.E, e1 = e0 + nrows;
+    if (e1 > g.flag_row0) {
+      if (tid == 0) {
+        const long lo = (e0 > g.flag_row0 ? e0 : g.flag_row0) - g.flag_row0, hi = e1 - 1 - g.flag_row0;
+        const unsigned need = (unsigned)(g.N / BN);
+        for (long r = lo / BM; r <= hi / BM; ++r) {
+          unsigned spins = 0;
+          while (__hip_atomic_load(g.flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&
+                 ++spins < (1u << 21))
+            __builtin_amdgcn_s_sleep(4);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+    }
+  }
+
   // ---- row exponents of the A chunks (edge layer 2): the lane's four rows
   int ex[4] = {0, 0, 0, 0};
   if (ASC) {
@@ -474,6 +497,17 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       all(Tr{});
     else
       all(F{});
+    if (g.flags) {
+      // k_edge16_tail: publish this tile (S rows + exponents) to the segment tiles of the same grid
+      // that read it: every wave's stores have reached L2, one agent-scope release writes the XCD's
+      // L2 back, then the tile's counter is bumped (one per column tile)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(g.flags + (row0 - g.flag_row0) / BM, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     stamp_end();
     return;
   }
@@ -573,10 +607,11 @@ __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
 }
 
 // Edge layer 1's partial last round and edge layer 2 in one grid: blocks [0, nb1) are layer-1 tiles
-// (g1, rows [g1.row_base, g1.M)), the rest layer-2 segment tiles (g2) that read none of those rows.
-// Workgroups are dispatched in index order, so the layer-1 tiles start first and the layer-2 tiles fill
-// the CUs they leave idle; nb1 is a multiple of 8 (blocks past the layer-1 tiles return at once), so
-// the layer-2 part keeps its XCD-aware tile order.
+// (g1, rows [g1.row_base, g1.M)), the rest are all of edge layer 2's segment tiles (g2). Workgroups
+// are dispatched in index order on every XCD, so the layer-1 tiles start first and the layer-2 tiles
+// fill the CUs they leave idle; the few segment tiles that read layer-1 rows of this grid (the last
+// ones of the tile order) wait for them through g1.flags / g2.flags (edge16_tile). nb1 is a multiple
+// of 8 (blocks past the layer-1 tiles return at once), so the layer-2 part keeps its XCD-aware order.
 __global__ __launch_bounds__(512, 1) void k_edge16_tail(EdgeArgs g1, EdgeArgs g2, int nb1, int nt1) {
   if ((int)blockIdx.x < nb1) {
     if ((int)blockIdx.x < nt1) edge16_tile<EPI_EDGE, false>(g1, blockIdx.x, nt1);
@@ -598,7 +633,8 @@ hipError_t edge16_init() {
 
 hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s) {
   if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
-      !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.M <= g1.row_base || g1.row_base < 0)
+      !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.M <= g1.row_base || g1.row_base < 0 ||
+      !g1.flags || g1.flags != g2.flags || g1.flag_row0 != g1.row_base || g2.flag_row0 != g1.row_base)
     return hipErrorInvalidValue;
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.tiles || g2.ntiles < 1 || !g2.agg || !g2.bias ||
       !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale)

@@ -46,6 +46,7 @@ struct LayerW {
 
 enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1, MATH_SPLIT16 = 2 };
 constexpr long kTileRows = 256;  // rows of the edge-GEMM tiles (gemm_bf16x3_big)
+constexpr int kMaxTailTiles = 512;  // layer-1 row tiles of a partial round (< CUs / 2)
 
 struct chm_model {
   chm_dims d;
@@ -64,7 +65,7 @@ struct chm_model {
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
-  int edge_split = 0;    // CHM_EDGE_SPLIT=1: partial-round tail split of edge layer 1 (see run_decoder)
+  int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int ncu = 0;           // compute units of the device the model lives on
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
@@ -90,10 +91,11 @@ struct chm_batch {
   void* owned = nullptr;  // the library's own allocation (chm_batch_create); null for caller workspaces
   size_t bytes = 0;
   // edge layer 1's partial last round (split16 / k_edge16, see run_decoder): rows [0, l1_rows_a) fill
-  // whole rounds of the grid; the rest runs in one grid with the segment tiles before l2_tile_a (which
-  // read none of those rows), the segment tiles from l2_tile_a on after it. 0 = no split.
+  // whole rounds of the grid; the rest runs in one grid with edge layer 2, whose segment tiles from
+  // l2_tile_a on read those rows. 0 = no split.
   long l1_rows_a = 0;
   int l2_tile_a = 0;
+  unsigned* tail_flags = nullptr;  // [kMaxTailTiles] per layer-1 row tile of the partial round
 };
 
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
@@ -343,6 +345,16 @@ extern "C" int chm_model_set_math(chm_model* m, int mode) {
 
 extern "C" int chm_model_get_math(const chm_model* m) { return m ? m->math : -1; }
 
+extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value) {
+  if (!m || !key) return fail(CHM_E_ARG, "NULL argument");
+  const std::string k = key;
+  if (k == "edge_split") {
+    m->edge_split = value != 0;
+    return CHM_OK;
+  }
+  return fail(CHM_E_ARG, "unknown option: " + k);
+}
+
 extern "C" void chm_model_destroy(chm_model* m) {
   if (!m) return;
   (void)hipFree(m->mem);
@@ -470,6 +482,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
   b->rmx = fl((size_t)4 * P * N);
+  b->tail_flags = (unsigned*)carve(kMaxTailTiles * sizeof(unsigned));
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
   b->LAT = fl((size_t)P * B * 9);
@@ -508,15 +521,17 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     return fail(CHM_E_ARG, "workspace too small or not 256-byte aligned (need " + std::to_string(need) + " bytes)");
   }
   b->bytes = batch_layout(b, m, base, b->ntiles);
-  {  // edge layer 1 tail split: whole rounds of 256x256 tiles first (needs ncu, an even count of tiles)
+  {  // edge layer 1 tail split: whole rounds of 256x256 tiles first (needs ncu, an even count of tiles).
+     // Only for a short partial round (<= 1/4 of the CUs): 64x40 (32 of 256 tiles) gains 6% per step;
+     // at 256x40 (128 of 256) the split grid lost 0.8% (profiles/r2/split_*)
     const long tiles1 = (t.E + kTileRows - 1) / kTileRows * (H / 256);
-    if (m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu) {
+    if (m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu && (tiles1 % m->ncu) * 4 <= m->ncu) {
       long full = tiles1 / m->ncu * m->ncu;
       full -= full % (H / 256);
       const long rows_a = full / (H / 256) * kTileRows;
       int ta = 0;
       while (ta < (int)t.tiles.size() && (t.tiles[ta].y < t.N ? t.estart[t.tiles[ta].y] : t.E) <= rows_a) ++ta;
-      if (rows_a < t.E && ta > 0 && ta < (int)t.tiles.size()) {
+      if (rows_a < t.E && ta > 0 && ta < (int)t.tiles.size() && (t.E - rows_a + kTileRows - 1) / kTileRows <= kMaxTailTiles) {
         b->l1_rows_a = rows_a;
         b->l2_tile_a = ta;
       }
@@ -765,20 +780,24 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       e2.node_estart = b->node_estart; e2.natoms = b->natoms; e2.n2g = b->n2g; e2.agg = b->agg;
       e2.node_n = b->node_n; e2.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
       e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
-      if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !g_prof_on && !m->edge_trace) {
+      // (instrumented eager launches keep one launch per layer, so the per-kernel timings stay whole;
+      // captured launches are never instrumented)
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+      if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !instrumented && !m->edge_trace) {
         // Edge layer 1 in whole rounds of the grid (rows [0, l1_rows_a)), then one grid with its
-        // partial last round first and edge layer 2's segment tiles that do not read those rows
-        // behind it, then the segment tiles that do. Same tiles, same arithmetic: bit-identical to
-        // one launch per layer.
-        EdgeArgs e1b = e1, e2b = e2;
+        // partial last round first and all of edge layer 2's segment tiles behind it (the few that
+        // read those rows wait for them inside the grid). Same tiles, same arithmetic: bit-identical
+        // to one launch per layer.
+        EdgeArgs e1b = e1;
         e1.M = b->l1_rows_a;
+        e1.zero_flags = b->tail_flags;
+        e1.nzero = (int)((E - b->l1_rows_a + kTileRows - 1) / kTileRows);
         e1b.row_base = b->l1_rows_a;
-        e2.ntiles = b->l2_tile_a;
-        e2b.tiles = b->tiles + b->l2_tile_a;
-        e2b.ntiles = b->ntiles - b->l2_tile_a;
+        e1b.flags = e2.flags = b->tail_flags;
+        e1b.flag_row0 = e2.flag_row0 = b->l1_rows_a;
         HIPCHK(edge_gemm16(e1, EPI_EDGE, s));
         HIPCHK(edge_gemm16_tail(e1b, e2, s));
-        HIPCHK(edge_gemm16(e2b, EPI_SEGMEAN, s));
       } else {
         {
           ProfScope ps(CHM_K_EDGE_FOURIER, s);

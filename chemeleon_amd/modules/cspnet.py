@@ -171,6 +171,7 @@ class CSPNet(nn.Module):
         self._hip_sig = None
         self._batches: Dict[Tuple, HipBatch] = {}
         self._math: Optional[str] = None  # set_math choice, re-applied when the packed weights are rebuilt
+        self._options: Dict[str, int] = {}  # set_option choices, likewise
         self._hip_lock = threading.RLock()
 
     # ------------------------------------------------------------------ HIP plumbing
@@ -206,7 +207,18 @@ class CSPNet(nn.Module):
                 if self._math is not None:
                     _lib.check(_lib.load().chm_model_set_math(self._hip.handle, _MATH_CODES[self._math]),
                                "chm_model_set_math")
+                for k, v in self._options.items():
+                    _lib.check(_lib.load().chm_model_set_option(self._hip.handle, k.encode(), int(v)),
+                               "chm_model_set_option")
             return self._hip
+
+    def set_option(self, key: str, value: int):
+        """Launch-schedule option of the C ABI (chm_model_set_option, e.g. 'edge_split'); results are
+        bit-identical either way. Survives rebuilds of the packed weights."""
+        with self._hip_lock:
+            _lib.check(_lib.load().chm_model_set_option(self.hip_model().handle, key.encode(), int(value)),
+                       "chm_model_set_option")
+            self._options[key] = int(value)
 
     def set_math(self, mode: str):
         """'split16' (default), 'bf16x3' or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h).

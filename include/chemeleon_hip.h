@@ -78,6 +78,13 @@ int chm_model_create(const chm_dims* dims, const float* const* d_params, int n_p
                      chm_model** out);
 void chm_model_destroy(chm_model* m);
 
+/* Launch-schedule options (results are bit-identical either way; not thread-safe against
+ * concurrent steps of the same model):
+ *   "edge_split" (0 / 1): when edge layer 1's 256x256 tiles leave a partial last round of the
+ *     grid, run that round in one grid with the edge-layer-2 tiles that do not read its rows.
+ * Returns CHM_E_ARG for an unknown key. */
+int chm_model_set_option(chm_model* m, const char* key, int64_t value);
+
 /* Arithmetic of the decoder GEMMs (all fp32-accurate, fp32 accumulation):
  *   CHM_MATH_SPLIT16 (default): the two edge GEMMs split each operand into an
  *     fp16 hi/lo pair (three fp16 MFMA products per fp32 product); W rows and

@@ -236,13 +236,14 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
         print(f"{tag} t={t}: types bit-exact ({N} atoms), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
 
 
-@pytest.mark.parametrize("nat", [[40] * 64, [40] * 256, [23, 7, 40, 1, 80] * 30])
-def test_edge_tail_split_is_bit_identical(model1000, cn, nat):
-    """When edge layer 1's 256x256 tiles do not fill whole rounds of the grid (64 x 40: 800 tiles on
-    256 CUs), the runtime runs the partial round on a forked stream beside edge layer 2 (runtime.hip,
-    run_decoder). Instrumented launches (chm_prof_enable) take the single-launch path, so the two
-    paths can be compared: one reverse step must agree bit for bit."""
-    lib = _lib.load()
+@pytest.mark.parametrize("nat", [[40] * 64, [50] * 40, [23, 7, 40, 1, 80] * 23])
+def test_edge_tail_split_is_bit_identical(cn, nat):
+    """When edge layer 1's 256x256 tiles leave a short partial round of the grid (64 x 40: 800 tiles
+    on 256 CUs), the runtime runs that round in one grid with edge layer 2, whose segment tiles that
+    read its rows wait for them inside the grid (runtime.hip run_decoder, option 'edge_split';
+    k_edge16_tail). Same tiles, same arithmetic: one reverse step must agree bit for bit with the
+    one-launch-per-layer schedule. Shapes: partial rounds of 32, 14 and 6 tiles (ragged: segment
+    tiles spanning crystals of 1-80 atoms wait on layer-1 tiles)."""
     B, N = len(nat), sum(nat)
     g = torch.Generator().manual_seed(11)
     a0 = torch.randint(0, 100, (N,), generator=g)
@@ -250,17 +251,15 @@ def test_edge_tail_split_is_bit_identical(model1000, cn, nat):
     l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
     nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
           torch.randn(N, 3, generator=g))
+    model = _model(1000)  # its own instance: the option stays out of the shared fixtures
     outs = []
-    for prof in (0, 1):
-        _lib.check(lib.chm_prof_enable(prof), "prof")
-        try:
-            outs.append([o.cpu() for o in model1000.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1],
-                                                                  noise=nz)])
-        finally:
-            _lib.check(lib.chm_prof_enable(0), "prof")
-            _lib.check(lib.chm_prof_reset(), "prof")
+    for split in (1, 0):
+        model.decoder.set_option("edge_split", split)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+    del model
+    torch.cuda.empty_cache()
     for u, v, what in zip(outs[0], outs[1], ("types", "frac", "lattice")):
-        assert torch.equal(u, v), f"{what}: split and single-launch edge layers differ"
+        assert torch.equal(u, v), f"{what}: split and one-launch-per-layer edge schedules differ"
 
 
 @pytest.mark.timeout(300)
