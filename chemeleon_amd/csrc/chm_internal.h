@@ -105,7 +105,6 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s);
 hipError_t node_gemm_init();
 extern int g_node_variant;  // microbenchmark probes of node_gemm (0 in the product)
 extern int g_node_blocks;   // S16 node GEMM blocks per CU override (microbenchmarks; 0 = default)
-extern int g_node_ks;       // S16 node GEMM K-interleave: 1 or 2 wave groups per tile
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
@@ -119,7 +118,10 @@ hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P,
 hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
                          int text_dim, float* cin, int B, int P, hipStream_t s);
 hipError_t decrement(int* d_t, hipStream_t s);
-hipError_t graph_bias(const float* lat, const float* Wc, long ldwc, const float* b1, float* out, int B, hipStream_t s);
+constexpr int kGBLayers = 16;
+struct GraphBiasArgs { const float* Wc[kGBLayers]; const float* b1[kGBLayers]; };
+// out[l] (l < nl, [B][H] each, consecutive) = the per-graph term of edge layer 1 of layer l
+hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldwc, float* out, int B, hipStream_t s);
 // rmx != null (split16 node GEMMs): rows of the four row-max arrays [4][rstride] (RMX_*): writes
 // max |Hl[row, :]| to RMX_HL and zeroes RMX_H, RMX_AGG, RMX_U for this layer's atomic maxima
 enum { RMX_H = 0, RMX_HL = 1, RMX_AGG = 2, RMX_U = 3 };

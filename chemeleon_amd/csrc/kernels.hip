@@ -328,25 +328,29 @@ hipError_t decrement(int* d_t, hipStream_t s) {
 }
 
 // per-graph part of the first edge layer: b1 + W1[:, 2H:2H+9] . vec(L L^T)
-__global__ void k_graph_bias(const float* __restrict__ lat, const float* __restrict__ Wc, long ldwc,
-                             const float* __restrict__ b1, float* __restrict__ out, int B) {
+// per-graph part of edge layer 1 for up to kGBLayers layers in one launch (blockIdx.y = layer):
+// out[l][g][n] = b1_l[n] + sum_ab W1_l[n, ab] (L L^T)_ab (cspnet.py:144-152, the C block of W1)
+__global__ void k_graph_bias(const float* __restrict__ lat, GraphBiasArgs a, long ldwc, float* __restrict__ out, int B) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)B * H) return;
+  const int l = blockIdx.y;
+  const float* Wc = a.Wc[l];
   const int gph = (int)(idx / H), n = (int)(idx % H);
   const float* L = lat + gph * 9;
-  float v = b1[n];
+  float v = a.b1[l][n];
 #pragma unroll
-  for (int a = 0; a < 3; ++a)
+  for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const float ip = L[a * 3 + 0] * L[b * 3 + 0] + L[a * 3 + 1] * L[b * 3 + 1] + L[a * 3 + 2] * L[b * 3 + 2];
-      v += Wc[n * ldwc + a * 3 + b] * ip;
+    for (int j = 0; j < 3; ++j) {
+      const float ip = L[i * 3 + 0] * L[j * 3 + 0] + L[i * 3 + 1] * L[j * 3 + 1] + L[i * 3 + 2] * L[j * 3 + 2];
+      v += Wc[n * ldwc + i * 3 + j] * ip;
     }
-  out[idx] = v;
+  out[(long)l * B * H + idx] = v;
 }
-hipError_t graph_bias(const float* lat, const float* Wc, long ldwc, const float* b1, float* out, int B, hipStream_t s) {
+hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldwc, float* out, int B, hipStream_t s) {
+  if (nl < 1 || nl > kGBLayers) return hipErrorInvalidValue;
   const long n = (long)B * H;
-  hipLaunchKernelGGL(k_graph_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lat, Wc, ldwc, b1, out, B);
+  hipLaunchKernelGGL(k_graph_bias, dim3((unsigned)((n + 255) / 256), nl), dim3(256), 0, s, lat, a, ldwc, out, B);
   return hipGetLastError();
 }
 

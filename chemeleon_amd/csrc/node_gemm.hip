@@ -46,10 +46,6 @@ constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
 template <bool S16> constexpr int STB = S16 ? A_STB + 2 * W_PLB : A_STB + 3 * W_PLB;
 // NB = blocks per CU: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of 16 KB)
 template <bool S16, int NB> constexpr int NST = NB == 3 ? 3 : (S16 ? 5 : 4);
-// KS = 2 (split16 only): 8 waves, the two groups of four take the even and odd K-tiles of the same
-// 128x128 tile (one stage = both groups' 16 KB sub-stages), their partial sums are added once
-// at the end (even + odd); one block per CU, 5 stages of 32 KB
-template <int KS, int NB> constexpr int NSTK = KS == 2 ? 5 : 0;
 constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
 static_assert(STB<true> * NST<true, 2> <= NODE_LDS && STB<false> * NST<false, 2> <= NODE_LDS, "LDS");
 static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
@@ -72,13 +68,13 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 }  // namespace
 
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR, bool S16, int NB, int KS = 1>
-__global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
-  static_assert((KS == 1 && (NB == 2 || (S16 && NB == 3))) || (KS == 2 && S16 && NB == 1), "blocks per CU");
-  constexpr int STB_ = STB<S16>, NST_ = KS == 2 ? NSTK<KS, NB> : NST<S16, NB>, AHEAD = NST_ - 1;  // stages in flight
+template <int VAR, bool S16, int NB>
+__global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
+  static_assert(NB == 2 || (S16 && NB == 3), "blocks per CU");
+  constexpr int STB_ = STB<S16>, NST_ = NST<S16, NB>, AHEAD = NST_ - 1;  // K-tiles in flight
   constexpr int GL = S16 ? 4 : 5;                                        // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, kh = (tid >> 6) >> 2, wave = (tid >> 6) & 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
   const int ntn = g.N / NN;
@@ -86,7 +82,7 @@ __global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
   const int n0 = (int)(bid % ntn) * NN;
   const long row0 = (bid / ntn) * NM;
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
-  const int nk = g.K / NK;  // K-tiles; this wave group takes tiles KS * t + kh, t < nk / KS
+  const int nk = g.K / NK;
 
   // ---- glds sources. A: instruction q (of 8) covers rows 16q + (L >> 2), LDS piece L & 3 holding
   // logical piece (L & 3) ^ ((L >> 4) & 3); wave w issues q = 2w, 2w + 1.
@@ -125,9 +121,8 @@ __global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
     }
   }
   auto issue = [&](int t) {
-    const int kt = KS * t + kh;
-    const int k0 = (kt < nk ? kt : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
-    char* st = lds + (t % NST_) * (KS * STB_) + kh * STB_;
+    const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
+    char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
@@ -179,7 +174,7 @@ __global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
   f32x4 ra0[2], ra1[2];
   frag fa[2][NP][2], fwt[2][NP][2];  // [set][part][i / j]
   auto read_raw = [&](int t, int set) {
-    const char* st = lds + (t % NST_) * (KS * STB_) + kh * STB_;
+    const char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       ra0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
@@ -289,44 +284,16 @@ __global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
     }
     __builtin_amdgcn_s_setprio(0);
   };
-  // nk / KS is even for every node GEMM (K = 512, 640, 1024; KS = 2: K = 512, 1024)
-  for (int t = 0; t < nk / KS; t += 2) {
+  for (int t = 0; t < nk; t += 2) {  // nk = K / 16 is even for every node GEMM (K = 512, 640, 1024)
     step(t, std::integral_constant<int, 0>{});
     step(t + 1, std::integral_constant<int, 1>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the block exits
-  if constexpr (KS == 2) {
-    // even + odd K-tile sums: group kh finishes row half i = kh; it sends its partial of row half
-    // 1 - kh through the (drained) ring and adds the other group's partial of row half kh
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    float* xb = reinterpret_cast<float*>(lds);
-    auto send = [&](auto I) __attribute__((always_inline)) {  // compile-time row half: acc stays in registers
-      constexpr int i = decltype(I)::value;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xb[((i * 4 + wave) * 32 + j * 16 + r) * 64 + lane] = acc[i][j][r];
-    };
-    auto add = [&](auto I) __attribute__((always_inline)) {
-      constexpr int i = decltype(I)::value;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] += xb[((i * 4 + wave) * 32 + j * 16 + r) * 64 + lane];
-    };
-    if (kh == 0) send(std::integral_constant<int, 1>{}); else send(std::integral_constant<int, 0>{});
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kh == 0) add(std::integral_constant<int, 0>{}); else add(std::integral_constant<int, 1>{});
-  }
 
   // lane l owns output row wm*64 + 32i + (l & 31) and, per 4-register group q, the four
   // consecutive columns wn*64 + 32j + 8q + 4h .. +3
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    if (KS == 2 && i != kh) continue;
     const long lr = wm * 64 + i * 32 + r32;
     float cm = 0.f;  // max |C| over this lane's columns of the row
     if (lr < nrows) {
@@ -362,23 +329,18 @@ __global__ __launch_bounds__(256 * KS, NB) void k_node_gemm(GemmArgs g) {
 
 int g_node_variant = 0;
 
-constexpr int LDSK2 = 2 * STB<true> * NSTK<2, 1>;
-static_assert(LDSK2 <= 160 * 1024, "LDS");
-
 hipError_t node_gemm_init() {
-  const void* ks[8] = {(const void*)k_node_gemm<0, false, 2>, (const void*)k_node_gemm<1, false, 2>,
+  const void* ks[6] = {(const void*)k_node_gemm<0, false, 2>, (const void*)k_node_gemm<1, false, 2>,
                        (const void*)k_node_gemm<0, true, 2>,  (const void*)k_node_gemm<1, true, 2>,
-                       (const void*)k_node_gemm<0, true, 3>,  (const void*)k_node_gemm<1, true, 3>,
-                       (const void*)k_node_gemm<0, true, 1, 2>, (const void*)k_node_gemm<1, true, 1, 2>};
+                       (const void*)k_node_gemm<0, true, 3>,  (const void*)k_node_gemm<1, true, 3>};
   constexpr int L3 = STB<true> * NST<true, 3>;
-  const int bytes[8] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, L3, L3, LDSK2, LDSK2};
+  const int bytes[6] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, L3, L3};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
-int g_node_ks = 1;      // S16 K-interleave (1 or 2 wave groups per tile)
 constexpr int LDS3 = STB<true> * NST<true, 3>;
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
@@ -398,10 +360,7 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
   // S16: three blocks per CU (3 stages each) once the grid fills a round of them: more waves to hide
   // the K-loop latency (-7% at M = 40960); small grids keep two blocks and 5 stages
   const int nb = g_node_blocks ? g_node_blocks : (blocks >= 3 * 256 ? 3 : 2);
-  if (g.wscale && g_node_ks == 2) {
-    if (g.K % (4 * NK) || g.ksplit % (2 * NK)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 1, 2> : k_node_gemm<0, true, 1, 2>), grid, dim3(512), LDSK2, s, g);
-  } else if (g.wscale && nb == 3)
+  if (g.wscale && nb == 3)
     hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3> : k_node_gemm<0, true, 3>), grid, block, LDS3, s, g);
   else if (g.wscale)
     hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 2> : k_node_gemm<0, true, 2>), grid, block, NODE_LDS, s, g);

@@ -246,8 +246,6 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (e16) m->edge16 = atoi(e16);
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
-    const char* nks = getenv("CHM_NODE_KS");
-    if (nks) g_node_ks = atoi(nks) == 2 ? 2 : 1;
     const char* spl = getenv("CHM_EDGE_SPLIT");
     if (spl) m->edge_split = atoi(spl);
     int dev = 0;
@@ -721,9 +719,11 @@ static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which
 }
 
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
+// reuse_cond: the FiLM conditioning (cond_in + the conditioning MLP) of the previous call on this batch
+// is still valid (same t and text: the corrector call of a reverse step, chemeleon.py:438-448)
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
                        int tstride, const int* d_t, const float* text0, const float* text1, int heads,
-                       hipStream_t s) {
+                       hipStream_t s, bool reuse_cond = false) {
   const chm_model* m = b->m;
   const int L = m->d.num_layers, X = m->d.text_dim, B = b->B;
   const long N = b->N, E = b->E, R = (long)P * N;
@@ -733,8 +733,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   const bool n16 = b->math == MATH_SPLIT16 && m->node16 && m->node_glds;
   const long RS = (long)b->P * N;
   auto rmx = [&](int k) { return n16 ? b->rmx + k * RS : nullptr; };
-  HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
-  {
+  if (!reuse_cond) {
+    HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
@@ -744,8 +744,15 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s));  // fp16 hi/lo planes [2][E][768] in F's bytes
   else
     HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
-  for (int l = 0; l < L; ++l)
-    HIPCHK(graph_bias(lat, m->layers[l].Wcl, 9, m->layers[l].b1, b->gbias + (size_t)l * B * H, B, s));
+  for (int l0 = 0; l0 < L; l0 += kGBLayers) {  // all layers' per-graph terms, one launch per 16 layers
+    GraphBiasArgs ga;
+    const int nl = L - l0 < kGBLayers ? L - l0 : kGBLayers;
+    for (int l = 0; l < nl; ++l) {
+      ga.Wc[l] = m->layers[l0 + l].Wcl;
+      ga.b1[l] = m->layers[l0 + l].b1;
+    }
+    HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
+  }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
     {  // FiLM projection (cspnet.py:92)
@@ -903,7 +910,8 @@ static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, fl
   sa.ra = ra; sa.rl = rl; sa.rx1 = rx1; sa.rx2 = rx2;
   sa.seed = seed; sa.node_base = node_base; sa.graph_base = graph_base;
   HIPCHK(step_predictor(sa, s));
-  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 1, s);
+  // corrector: same t and text as the predictor, so its FiLM conditioning is reused
+  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 1, s, true);
   if (rc) return rc;
   HIPCHK(step_corrector(sa, s));
   if (d_t) HIPCHK(decrement(d_t, s));

@@ -35,6 +35,8 @@ __global__ void split_h(const float* x, long n, _Float16* out) {  // split rows 
   out[o + 32] = (_Float16)(x[i] - (float)h);
 }
 
+__global__ void k_empty() {}
+
 __global__ void fill(float* p, long n, unsigned seed, float scale) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -167,29 +169,30 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  if (argc > 3 && std::string(argv[3]) == "nodeks") {  // split16 node GEMM: K-interleave 1 vs 2 wave groups
+  if (argc > 3 && std::string(argv[3]) == "nodefix") {  // split16 node GEMM time vs K (fixed cost = intercept)
     CK(node_gemm_init());
     void* W16; float* wsc16; float* amax;
     CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
     CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
     std::vector<float> one(M, 1.0f);
     CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
-    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax;
-    const size_t nc = (size_t)std::min<long>(M, 8192) * N;
-    std::vector<float> ref(nc), c(nc);
-    CK(gemm(g, EPI_STD, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(ref.data(), C, nc * 4, hipMemcpyDeviceToHost));
-    for (int rep = 0; rep < 3; ++rep)
-      for (int ks : {1, 2}) {
-        g_node_ks = ks;
-        float t = time_it(20, s, [&] { CK(node_gemm(g16, s)); });
-        CK(hipMemcpy(c.data(), C, nc * 4, hipMemcpyDeviceToHost));
-        double e = 0, r = 0;
-        for (size_t i = 0; i < nc; ++i) { e = fmax(e, fabs((double)c[i] - ref[i])); r = fmax(r, fabs((double)ref[i])); }
-        printf("M=%ld N=%d K=%d  KS=%d: %.1f us %.1f TF  max err vs f32 MFMA %.2e (max |C| %.2e)\n", M, N, K, ks,
-               t * 1e3, flops / t / 1e9, e, r);
+    for (int rep = 0; rep < 2; ++rep)
+      for (int k = 64; k <= K; k *= 2) {
+        GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax; g16.K = k; g16.ksplit = k;
+        g16.lda = K; g16.lda2 = K;
+        float t = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+        GemmArgs g0 = g16; g0.bias = nullptr; g0.act = 0;
+        float t0 = time_it(50, s, [&] { CK(node_gemm(g0, s)); });
+        g_node_blocks = 2;
+        float t2 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+        g_node_blocks = 3;
+        float t3 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+        g_node_blocks = 0;
+        printf("M=%ld N=%d K=%d: default %.2f us (no bias/act %.2f us) | 2 blocks/CU %.2f us | 3 blocks/CU %.2f us\n", M,
+               N, k, t * 1e3, t0 * 1e3, t2 * 1e3, t3 * 1e3);
       }
-    g_node_ks = 1;
+    float te = time_it(50, s, [&] { hipLaunchKernelGGL(k_empty, dim3(160), dim3(256), 0, s); });
+    printf("empty kernel, 160 blocks: %.2f us per launch\n", te * 1e3);
     return 0;
   }
   if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
