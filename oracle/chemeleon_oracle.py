@@ -176,15 +176,19 @@ def _ln(x, sd, p):
 
 def cspnet_forward(sd: Dict[str, torch.Tensor], cfg: Dict, atom_types, frac_coords, lattices,
                    num_atoms, node2graph, t_emb=None, text=None, hidden: Optional[List] = None):
-    """cspnet.py:345-405 (fc edges, ln, ip, smooth=False).
+    """cspnet.py:345-405 (ln, ip, smooth=False; cfg["edge_style"] "fc" (default) or "knn").
 
     Returns (type_logits [N,A], lattice_out [B,3,3], coords_out [N,3],
     node_features [N,H]). If `hidden` is a list, the node features after
     each layer are appended to it."""
     silu = F.silu
     natoms = [int(n) for n in num_atoms]
-    edges = fc_edges(natoms)
-    frac_diff = (frac_coords[edges[1]] - frac_coords[edges[0]]) % 1.0  # cspnet.py:324
+    if cfg.get("edge_style", "fc") == "knn":  # cspnet.py:325-343 (oracle/knn_oracle.py)
+        from oracle.knn_oracle import knn_edges
+        edges, frac_diff = knn_edges(natoms, frac_coords, lattices, cfg.get("max_neighbors", 20))
+    else:
+        edges = fc_edges(natoms)
+        frac_diff = (frac_coords[edges[1]] - frac_coords[edges[0]]) % 1.0  # cspnet.py:324
     e2g = node2graph[edges[0]]  # :356
     h = F.embedding(atom_types, sd["node_embedding.weight"])  # :357
     t_atom = t_emb.repeat_interleave(num_atoms, dim=0) if t_emb is not None else None  # :360

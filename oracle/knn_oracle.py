@@ -1,0 +1,145 @@
+"""ORACLE (test infrastructure only; never imported by the product path): the reference's
+optional radius-graph edge mode, `CSPNet(edge_style="knn")`, restated on the CPU in PyTorch fp32.
+
+What it restates (paths relative to the reference repo root):
+* `radius_graph_pbc` (chemeleon/utils/data_utils.py:151-316): all atom pairs of a crystal against the
+  27 neighbouring cells (max_rep = 1 per axis), radius = smallest interplanar spacing + 0.01,
+  pairs with d^2 <= r^2 and d^2 > 1e-4 kept in (atom1, atom2, cell) order;
+* `get_max_neighbors_mask` (data_utils.py:319-398): when some atom has more than
+  `max_num_neighbors_threshold` kept pairs, every atom keeps the pairs with
+  d^2 < (its (threshold+1)-th smallest d^2) + 0.01 (ties and near-ties included);
+* `CSPNet.reorder_symmetric_edges` / `select_symmetric_edges` / `gen_edges` (cspnet.py:236-343):
+  one direction of every pair (index2 < index1, or the same atom with an "earlier" cell), then per
+  crystal those edges followed by their reverses; frac_diff = -(x[j] - x[i] + cell) for the kept
+  direction and +(...) for the reverse (no `% 1.0`).
+
+The reference path cannot run as shipped: `segment_coo` / `segment_csr` (torch_scatter, absent from
+the image and with its import commented out, data_utils.py:7) raise NameError. They are
+sum reductions over sorted indices / CSR pointers; `segment_coo` and `segment_csr` below restate
+torch_scatter's published semantics (reduce="sum"), and tests/golden/make_golden.py injects the same
+two functions into the unmodified reference module to write the knn fixtures that pin this file.
+"""
+
+from typing import Sequence, Tuple
+
+import torch
+
+
+def segment_coo(src: torch.Tensor, index: torch.Tensor, dim_size: int) -> torch.Tensor:
+    """torch_scatter.segment_coo(src, index, dim_size=..., reduce="sum") for 1-D sorted `index`."""
+    out = torch.zeros(dim_size, dtype=src.dtype)
+    return out.index_add_(0, index, src.expand_as(index).to(src.dtype))
+
+
+def segment_csr(src: torch.Tensor, indptr: torch.Tensor) -> torch.Tensor:
+    """torch_scatter.segment_csr(src, indptr, reduce="sum") for 1-D `src`."""
+    c = torch.cat([src.new_zeros(1), torch.cumsum(src, 0)])
+    return c[indptr[1:]] - c[indptr[:-1]]
+
+
+def _unit_cells() -> torch.Tensor:
+    """data_utils.py:234-242: meshgrid (ij) of [-1, 0, 1]^3, rows (a, b, c) with c fastest."""
+    r = torch.arange(-1, 2, dtype=torch.float)
+    return torch.cat([g.reshape(-1, 1) for g in torch.meshgrid(r, r, r, indexing="ij")], dim=-1)
+
+
+def radius_graph_pbc(pos: torch.Tensor, cell: torch.Tensor, natoms: torch.Tensor, max_nb: int):
+    """data_utils.py:151-316. Returns (edge_index [2, E] = (index2, index1), unit cell of index2
+    [E, 3] (float), kept-neighbour count per crystal [B])."""
+    B = len(natoms)
+    nsq = natoms ** 2
+    ioff = torch.cumsum(natoms, 0) - natoms
+    ioff_x = torch.repeat_interleave(ioff, nsq)
+    n_x = torch.repeat_interleave(natoms, nsq)
+    sqoff = torch.repeat_interleave(torch.cumsum(nsq, 0) - nsq, nsq)
+    cnt = torch.arange(int(nsq.sum())) - sqoff
+    index1 = torch.div(cnt, n_x, rounding_mode="floor") + ioff_x
+    index2 = cnt % n_x + ioff_x
+    pos1 = torch.index_select(pos, 0, index1)
+    pos2 = torch.index_select(pos, 0, index2)
+    # interplanar spacings (data_utils.py:202-219)
+    c23 = torch.cross(cell[:, 1], cell[:, 2], dim=-1)
+    vol = torch.sum(cell[:, 0] * c23, dim=-1, keepdim=True)
+    d1 = (1 / torch.norm(c23 / vol, p=2, dim=-1)).reshape(-1, 1)
+    c31 = torch.cross(cell[:, 2], cell[:, 0], dim=-1)
+    d2 = (1 / torch.norm(c31 / vol, p=2, dim=-1)).reshape(-1, 1)
+    c12 = torch.cross(cell[:, 0], cell[:, 1], dim=-1)
+    d3 = (1 / torch.norm(c12 / vol, p=2, dim=-1)).reshape(-1, 1)
+    min_dist = torch.cat([d1, d2, d3], dim=-1)
+    uc = _unit_cells()
+    ncell = len(uc)
+    uc_atom = uc.view(1, ncell, 3).repeat(len(index2), 1, 1)
+    uc_b = torch.transpose(uc, 0, 1).view(1, 3, ncell).expand(B, -1, -1)
+    offs = torch.bmm(torch.transpose(cell, 1, 2), uc_b)  # data_utils.py:252-254
+    offs_atom = torch.repeat_interleave(offs, nsq, dim=0)
+    pos1 = pos1.view(-1, 3, 1).expand(-1, -1, ncell)
+    pos2 = pos2.view(-1, 3, 1).expand(-1, -1, ncell) + offs_atom
+    index1 = index1.view(-1, 1).repeat(1, ncell).view(-1)
+    index2 = index2.view(-1, 1).repeat(1, ncell).view(-1)
+    d2s = torch.sum((pos1 - pos2) ** 2, dim=1).view(-1)
+    r = min_dist.min(dim=-1)[0] + 0.01  # data_utils.py:272
+    r = torch.repeat_interleave(r, nsq * ncell)
+    keep = torch.le(d2s, r * r) & torch.gt(d2s, 0.0001)
+    index1, index2 = index1[keep], index2[keep]
+    uc_k = uc_atom.view(-1, 3)[keep]
+    d2s = d2s[keep]
+    nbmask, nb_image = max_neighbors_mask(natoms, index1, d2s, max_nb)
+    if not torch.all(nbmask):
+        index1, index2, uc_k = index1[nbmask], index2[nbmask], uc_k[nbmask]
+    return torch.stack((index2, index1)), uc_k, nb_image
+
+
+def max_neighbors_mask(natoms: torch.Tensor, index: torch.Tensor, d2: torch.Tensor, thr: int):
+    """data_utils.py:319-398 (index sorted). Returns (keep mask [E], kept count per crystal [B])."""
+    num_atoms = int(natoms.sum())
+    nnb = segment_coo(torch.ones(1, dtype=torch.long), index, num_atoms)
+    max_nb = int(nnb.max()) if len(nnb) else 0
+    indptr = torch.zeros(len(natoms) + 1, dtype=torch.long)
+    indptr[1:] = torch.cumsum(natoms, 0)
+    per_image = segment_csr(nnb.clamp(max=thr), indptr)
+    if max_nb <= thr or thr <= 0:
+        return torch.ones(len(index), dtype=torch.bool), per_image
+    dsort = torch.full([num_atoms * max_nb], float("inf"))
+    off = torch.cumsum(nnb, 0) - nnb
+    slot = index * max_nb + torch.arange(len(index)) - torch.repeat_interleave(off, nnb)
+    dsort.index_copy_(0, slot, d2)
+    dsort, isort = torch.sort(dsort.view(num_atoms, max_nb), dim=1)
+    cutoff = dsort[:, thr].reshape(-1, 1).expand(-1, max_nb) + 0.01
+    ok = torch.isfinite(dsort) & (dsort < cutoff)
+    isort = (isort + off.view(-1, 1).expand(-1, max_nb))[ok]
+    per_image = segment_csr(ok.sum(dim=-1), indptr)
+    mask = torch.zeros(len(index), dtype=torch.bool)
+    mask.index_fill_(0, isort, True)
+    return mask, per_image
+
+
+def knn_edges(natoms: Sequence[int], frac: torch.Tensor, lattices: torch.Tensor, max_nb: int = 20
+              ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cspnet.py:325-343 + reorder_symmetric_edges (:255-317): (edge_index [2, E], frac_diff [E, 3])."""
+    nat = torch.as_tensor([int(n) for n in natoms])
+    n2g = torch.arange(len(nat)).repeat_interleave(nat)
+    cart = torch.einsum("bi,bij->bj", frac, lattices[n2g])
+    ei, img, nb = radius_graph_pbc(cart, lattices, nat, max_nb)
+    j_index, i_index = ei
+    ev = frac[j_index] - frac[i_index]
+    ev += img.float()
+    # one direction of every pair (cspnet.py:273-292)
+    sep = ei[0] < ei[1]
+    earlier = (img[:, 0] < 0) | ((img[:, 0] == 0) & (img[:, 1] < 0)) | ((img[:, 0] == 0) & (img[:, 1] == 0) & (img[:, 2] < 0))
+    keep = sep | ((ei[0] == ei[1]) & earlier)
+    d_idx = ei[:, keep]
+    d_ev = ev[keep]
+    # per crystal: its kept edges, then their reverses (:294-317; repeat_blocks with repeats = 2)
+    per = torch.bincount(torch.repeat_interleave(torch.arange(len(nat)), nb)[keep], minlength=len(nat))
+    starts = torch.cumsum(per, 0) - per
+    idx_all, ev_all = [], []
+    for b in range(len(nat)):
+        s, c = int(starts[b]), int(per[b])
+        if c == 0:
+            continue
+        fwd = d_idx[:, s:s + c]
+        idx_all.append(torch.cat([fwd, torch.stack([fwd[1], fwd[0]])], dim=1))
+        ev_all.append(torch.cat([d_ev[s:s + c], -d_ev[s:s + c]]))
+    if not idx_all:
+        return torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, 3)
+    return torch.cat(idx_all, dim=1), -torch.cat(ev_all)

@@ -373,6 +373,81 @@ def reference_single_step(m, natoms, a, x, lat, t, noise_seed):
     return captured["s"]
 
 
+def _inject_segment_ops():
+    """The reference's knn path calls torch_scatter.segment_coo / segment_csr, whose import is
+    commented out (chemeleon/utils/data_utils.py:7): as shipped it raises NameError. This harness
+    injects the two sum reductions (torch_scatter semantics, reduce="sum": segment_coo sums src into
+    dim_size slots by sorted index, segment_csr sums src between CSR pointers) into the unmodified
+    module, so the reference's own radius_graph_pbc / get_max_neighbors_mask / symmetric reorder run."""
+    import chemeleon.utils.data_utils as dutil
+
+    def segment_coo(src, index, dim_size=None, reduce="sum"):
+        assert reduce == "sum"
+        n = int(index.max()) + 1 if dim_size is None else int(dim_size)
+        out = torch.zeros(n, dtype=src.dtype)
+        for k, v in zip(index.tolist(), src.expand_as(index).tolist()):
+            out[k] += v
+        return out
+
+    def segment_csr(src, indptr, reduce="sum"):
+        assert reduce == "sum"
+        p = indptr.tolist()
+        return torch.stack([src[p[k]:p[k + 1]].sum() for k in range(len(p) - 1)]).to(src.dtype)
+
+    dutil.segment_coo, dutil.segment_csr = segment_coo, segment_csr
+    return dutil
+
+
+def knn_crystals(natoms, seed, a_lo, a_hi):
+    """Random well-conditioned cells (edge lengths in [a_lo, a_hi] Angstrom, shear up to 0.3) and
+    uniform fractional coordinates."""
+    g = torch.Generator().manual_seed(seed)
+    B, N = len(natoms), sum(natoms)
+    x = torch.rand(N, 3, generator=g)
+    diag = a_lo + (a_hi - a_lo) * torch.rand(B, 3, generator=g)
+    lat = torch.diag_embed(diag) + 0.3 * (torch.rand(B, 3, 3, generator=g) - 0.5) * diag.mean(1).view(B, 1, 1)
+    a = torch.randint(1, 104, (N,), generator=g)
+    return a, x, lat
+
+
+KNN_CASES = (("small", [3, 5, 8, 1, 12], 31, 4.0, 7.0), ("dense", [40, 24], 32, 5.0, 7.0),
+             ("uncapped", [2, 4, 3], 33, 3.0, 5.0))
+
+
+def gen_knn(chm, csp):
+    """edge_style='knn' (SURVEY a17): the reference's gen_edges (radius_graph_pbc + max-neighbour mask +
+    symmetric reorder) with the segment ops injected, the intermediate radius graph, and decoder
+    outputs of the knn CSPNet (synthetic weights) at t = 500."""
+    dutil = _inject_segment_ops()
+    m, sd = build_reference_model(chm, csp, 1000)
+    dec = csp.CSPNet(hidden_dim=512, time_dim=128, text_dim=512, num_layers=6, max_atoms=104, act_fn="silu",
+                     dis_emb="sin", num_freqs=128, edge_style="knn", cutoff=6.0, max_neighbors=20, ln=True,
+                     ip=True, smooth=False, pred_atom_types=True)
+    dec.load_state_dict(sd)
+    dec = dec.eval()
+    rec = {"weights_crc": weights_crc(sd)}
+    cond, _ = synthetic_text_embeds(512)
+    for tag, natoms, seed, a_lo, a_hi in KNN_CASES:
+        a, x, lat = knn_crystals(natoms, seed, a_lo, a_hi)
+        B = len(natoms)
+        nat = torch.tensor(natoms)
+        n2g = torch.arange(B).repeat_interleave(nat)
+        cart = torch.einsum("bi,bij->bj", x, lat[n2g])
+        ei, img, nb = dutil.radius_graph_pbc(pos=cart, cell=lat, natoms=nat, max_num_neighbors_threshold=20)
+        edges, fd = dec.gen_edges(nat, x, lat, n2g)
+        te = m.time_embed(torch.full((B,), 500, dtype=torch.long))
+        with torch.no_grad():
+            o = dec(atom_types=a, frac_coords=x, lattices=lat, num_atoms=nat, node2graph=n2g, t=te,
+                    text_embeds=cond.expand(B, -1))
+        rec.update({f"{tag}_natoms": nat, f"{tag}_atom_types": a, f"{tag}_frac": x, f"{tag}_lattices": lat,
+                    f"{tag}_radius_edges": ei, f"{tag}_radius_images": img, f"{tag}_radius_counts": nb,
+                    f"{tag}_edges": edges, f"{tag}_frac_diff": fd, f"{tag}_types": o.atom_types_out,
+                    f"{tag}_coords": o.coords_out, f"{tag}_lattice_out": o.lattice_out,
+                    f"{tag}_node_features": o.node_features})
+        print(tag, "radius pairs", ei.shape[1], "edges", edges.shape[1])
+    save("knn.npz", **rec)
+
+
 def _run_reference_trajectory(m, T, every):
     from chemeleon.modules import schema
     states = []
@@ -524,5 +599,7 @@ if __name__ == "__main__":
         gen_state_keys(chm, csp)
     if "text" in which:
         gen_text(chm, csp)
+    if "knn" in which:
+        gen_knn(chm, csp)
     if "trajectory1000" in which:
         gen_trajectory(chm, csp, T=1000, every=10)
