@@ -29,6 +29,14 @@ class chm_dims(ctypes.Structure):
                 ("max_atoms", c_int), ("num_freqs", c_int)]
 
 
+class chm_batch_options(ctypes.Structure):
+    _fields_ = [("edge_style", ctypes.c_int32), ("max_neighbors", ctypes.c_int32),
+                ("knn_edges_per_atom", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+EDGES_FC, EDGES_KNN = 0, 1
+
+
 class chm_schedule(ctypes.Structure):
     _fields_ = [("T", c_int), ("d_coef", c_void_p), ("d_time_emb", c_void_p), ("d_q_one_step", c_void_p),
                 ("d_q_mats", c_void_p)]
@@ -50,6 +58,13 @@ SIGNATURES = {
     "chm_batch_workspace_bytes": (ctypes.c_size_t, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int]),
     "chm_batch_create_with_workspace": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int, c_void_p,
                                                 ctypes.c_size_t, c_void_p, ctypes.POINTER(c_void_p)]),
+    "chm_batch_workspace_bytes_ex": (ctypes.c_size_t, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int,
+                                                       ctypes.POINTER(chm_batch_options)]),
+    "chm_batch_create_ex": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int,
+                                    ctypes.POINTER(chm_batch_options), c_void_p, ctypes.c_size_t, c_void_p,
+                                    ctypes.POINTER(c_void_p)]),
+    "chm_knn_edges": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
+                              ctypes.POINTER(c_i64), c_void_p]),
     "chm_debug_philox": (c_int, [c_u64, c_int, c_int, c_i64, c_i64, c_int, c_void_p, c_void_p]),
     "chm_debug_d3pm_philox": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_u64,
                                       c_i64, c_void_p, c_void_p]),

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libchemeleon_hip.so")
-SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "edge_gemm.hip", "edge16.hip", "node_gemm.hip", "runtime.hip"]
+SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "edge_gemm.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip"]
 ARCH = os.environ.get("CHM_OFFLOAD_ARCH", "gfx950")
 
 

@@ -80,6 +80,16 @@ struct EdgeArgs {
             // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
             // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN)
 };
+// knn (radius-graph) edges, knn.hip: per-crystal scratch at cand_off[b] (n^2 * 27 entries; the final
+// list at 2 * cand_off[b]), outputs sorted by source node into ei / ej / fd at node_estart
+struct KnnArgs {
+  const float* x; const float* lat; const int* natoms; const int* node_off;
+  const long* cand_off; unsigned* cand_key; float* cand_d2; unsigned* cand2; int* atom_cnt; int max_nb;
+  unsigned* fin_key; float* fin_fd; int* deg; int* cryst_fin;
+  const long* node_estart; int* ei; int* ej; float* fd;
+};
+hipError_t knn_candidates(const KnnArgs& g, int B, hipStream_t s);  // pairs, cap, symmetric list, degrees
+hipError_t knn_place(const KnnArgs& g, int B, hipStream_t s);       // grouped by source (node_estart set)
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
 // the same kernels on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)
@@ -91,7 +101,8 @@ hipError_t edge16_init();
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);
-hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s);
+hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s,
+                     const float* fd = nullptr);
 
 hipError_t gemm(const GemmArgs& g, int epi, hipStream_t s);
 // fp32-accurate GEMM on bf16 MFMA: A split on the fly into hi/mid/lo bf16,

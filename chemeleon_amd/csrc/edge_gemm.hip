@@ -807,17 +807,23 @@ hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, 
 
 // Fourier features (cspnet.py:38-52 as k_fourier) written split, rows [768/32][hi 32 | lo 32].
 // One thread per (edge, axis, 8 consecutive frequencies): 8 sincosf, four 16-B stores.
+// fd != null (knn edges): the edge's displacement is given (cspnet.py:342-343, no % 1.0)
 __global__ __launch_bounds__(256) void k_fourier_h(const float* __restrict__ x, const int* __restrict__ ei,
-                                                   const int* __restrict__ ej, long E, _Float16* __restrict__ F) {
+                                                   const int* __restrict__ ej, const float* __restrict__ fd, long E,
+                                                   _Float16* __restrict__ F) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   constexpr int G = NF / 8;  // groups of 8 frequencies per axis
   if (idx >= E * 3 * G) return;
   const long e = idx / (3 * G);
   const int r = (int)(idx - e * 3 * G);
   const int a = r / G, k0 = (r - a * G) * 8;
-  // torch.remainder(d, 1.0): fmod, negatives shifted by +1 (k_fourier's rem1)
-  float d = fmodf(__fsub_rn(x[(long)ej[e] * 3 + a], x[(long)ei[e] * 3 + a]), 1.0f);
-  if (d < 0.0f) d = __fadd_rn(d, 1.0f);
+  float d;
+  if (fd) {
+    d = fd[e * 3 + a];
+  } else {  // torch.remainder(d, 1.0): fmod, negatives shifted by +1 (k_fourier's rem1)
+    d = fmodf(__fsub_rn(x[(long)ej[e] * 3 + a], x[(long)ei[e] * 3 + a]), 1.0f);
+    if (d < 0.0f) d = __fadd_rn(d, 1.0f);
+  }
   f16x8 sh, sl, ch, cl;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
@@ -837,9 +843,10 @@ __global__ __launch_bounds__(256) void k_fourier_h(const float* __restrict__ x, 
   *reinterpret_cast<f16x8*>(f + (cc / 32) * 64 + 32 + cc % 32) = cl;
 }
 
-hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s) {
+hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s, const float* fd) {
   const long n = E * 3 * (NF / 8);
-  hipLaunchKernelGGL(k_fourier_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ei, ej, E,
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fourier_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ei, ej, fd, E,
                      reinterpret_cast<_Float16*>(F));
   return hipGetLastError();
 }

@@ -96,6 +96,17 @@ struct chm_batch {
   long l1_rows_a = 0;
   int l2_tile_a = 0;
   unsigned* tail_flags = nullptr;  // [kMaxTailTiles] per layer-1 row tile of the partial round
+  // knn (radius-graph) batches: edges rebuilt every decoder call (knn.hip); E is then the current
+  // graph's edge count and E_cap the capacity the edge buffers are sized for
+  int knn = 0, knn_max_nb = 20;
+  long E_cap = 0, C_cap = 0;
+  long* cand_off = nullptr;
+  unsigned *cand_key = nullptr, *cand2 = nullptr, *fin_key = nullptr;
+  float *cand_d2 = nullptr, *fin_fd = nullptr, *fd = nullptr;
+  int *atom_cnt = nullptr, *deg = nullptr, *cryst_fin = nullptr;
+  std::vector<int> h_deg, h_fin;
+  std::vector<long> h_estart;
+  std::vector<int2> h_tiles;
 };
 
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
@@ -365,14 +376,30 @@ extern "C" void chm_model_destroy(chm_model* m) {
 // Host-side index tables of a batch (the implicit fc edge layout) and the byte layout of its
 // device memory: index tables first, then the decoder workspace, each piece 256-byte aligned.
 // The same carve() sequence sizes the block (base == null) and binds a batch to it.
-struct BatchTables {
-  std::vector<int> nat, noff, n2g, ei, ej, nn;
-  std::vector<long> eoff, estart;
-  std::vector<int2> tiles;
-  long N = 0, E = 0;
+struct BatchOpts {
+  int knn = 0, max_nb = 20, per_atom = 128;
 };
 
-static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t) {
+static int batch_opts(const chm_batch_options* o, BatchOpts& bo) {
+  if (!o) return CHM_OK;
+  if (o->edge_style != CHM_EDGES_FC && o->edge_style != CHM_EDGES_KNN) return fail(CHM_E_ARG, "unknown edge_style");
+  bo.knn = o->edge_style == CHM_EDGES_KNN;
+  if (o->max_neighbors) bo.max_nb = o->max_neighbors;
+  if (o->knn_edges_per_atom) bo.per_atom = o->knn_edges_per_atom;
+  if (bo.per_atom < 1 || bo.per_atom > 4096) return fail(CHM_E_ARG, "knn_edges_per_atom out of range");
+  return CHM_OK;
+}
+
+struct BatchTables {
+  std::vector<int> nat, noff, n2g, ei, ej, nn;
+  std::vector<long> eoff, estart, coff;
+  std::vector<int2> tiles;
+  long N = 0, E = 0;  // knn: E = the edge capacity
+  long C = 0;         // knn: candidate scratch entries (sum of n^2 * 27)
+  bool knn = false;
+};
+
+static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t, const BatchOpts& bo = BatchOpts()) {
   t.nat.assign(h_natoms, h_natoms + B);
   t.noff.assign(B + 1, 0);
   t.eoff.assign(B + 1, 0);
@@ -390,6 +417,14 @@ static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t) {
   t.eoff[B] = E;
   t.N = N;
   t.E = E;
+  t.knn = bo.knn;
+  if (bo.knn) {  // radius graph: candidates n^2 * 27 per crystal, edges up to per_atom per atom
+    t.coff.assign(B + 1, 0);
+    for (int g = 0; g < B; ++g) t.coff[g + 1] = t.coff[g] + (long)t.nat[g] * t.nat[g] * 27;
+    t.C = t.coff[B];
+    t.E = N * (long)bo.per_atom;
+    if (t.E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
+  }
   return CHM_OK;
 }
 
@@ -398,15 +433,17 @@ static void batch_fill(BatchTables& t) {
   const int B = (int)t.nat.size();
   const long N = t.N, E = t.E;
   t.n2g.resize(N);
-  t.ei.resize(E);
-  t.ej.resize(E);
   t.nn.resize(N);
-  t.estart.resize(N);
-  for (int g = 0; g < B; ++g) {
+  for (int g = 0; g < B; ++g)
     for (int i = 0; i < t.nat[g]; ++i) {
       t.n2g[t.noff[g] + i] = g;
       t.nn[t.noff[g] + i] = t.nat[g];
     }
+  if (t.knn) return;  // (edge tables are built per decoder call)
+  t.ei.resize(E);
+  t.ej.resize(E);
+  t.estart.resize(N);
+  for (int g = 0; g < B; ++g) {
     long e = t.eoff[g];
     for (int i = 0; i < t.nat[g]; ++i)
       for (int j = 0; j < t.nat[g]; ++j, ++e) {
@@ -434,6 +471,7 @@ static void batch_fill(BatchTables& t) {
 
 // number of segment tiles without building the tables (sizing only)
 static long count_tiles(const BatchTables& t) {
+  if (t.knn) return t.N + 1;
   long n = 1, rows = 0;
   for (size_t g = 0; g < t.nat.size(); ++g)
     for (int i = 0; i < t.nat[g]; ++i) {
@@ -466,6 +504,18 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->node_estart = (long*)carve(N * sizeof(long));
   b->node_n = (int*)carve(N * sizeof(int));
   b->tiles = (int2*)carve(ntiles * sizeof(int2));
+  if (b->knn) {  // (E = the edge capacity E_cap)
+    b->cand_off = (long*)carve((B + 1) * sizeof(long));
+    b->cand_key = (unsigned*)carve(b->C_cap * sizeof(unsigned));
+    b->cand2 = (unsigned*)carve(b->C_cap * sizeof(unsigned));
+    b->cand_d2 = (float*)carve(b->C_cap * sizeof(float));
+    b->fin_key = (unsigned*)carve(2 * b->C_cap * sizeof(unsigned));
+    b->fin_fd = (float*)carve(6 * b->C_cap * sizeof(float));
+    b->fd = (float*)carve(3 * E * sizeof(float));
+    b->atom_cnt = (int*)carve(N * sizeof(int));
+    b->deg = (int*)carve(N * sizeof(int));
+    b->cryst_fin = (int*)carve(B * sizeof(int));
+  }
   b->cin = fl((size_t)P * B * (TD + X));
   b->cemb = fl((size_t)P * B * 2 * H);
   b->Hres = fl((size_t)P * N * H);
@@ -488,13 +538,15 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
 }
 
 static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, void* d_ws,
-                       size_t ws_bytes, hipStream_t s, chm_batch** out) {
+                       size_t ws_bytes, hipStream_t s, chm_batch** out, const BatchOpts& bo = BatchOpts()) {
   if (!out) return fail(CHM_E_ARG, "out is NULL");
   *out = nullptr;
   if (!m || !h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   if (max_pairs < 1 || max_pairs > 2) return fail(CHM_E_ARG, "max_pairs must be 1 or 2");
+  if (bo.knn && (m->math != MATH_SPLIT16 || !m->edge16))
+    return fail(CHM_E_UNSUPPORTED, "knn edges need the split16 arithmetic on the k_edge16 kernels");
   BatchTables t;
-  int rc = batch_tables(h_natoms, B, t);
+  int rc = batch_tables(h_natoms, B, t, bo);
   if (rc) return rc;
   batch_fill(t);
   chm_batch* b = new chm_batch();
@@ -505,7 +557,11 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->N = t.N;
   b->E = t.E;
   b->h_natoms = t.nat;
-  b->ntiles = (int)t.tiles.size();
+  b->knn = bo.knn;
+  b->knn_max_nb = bo.max_nb;
+  b->E_cap = t.E;
+  b->C_cap = t.C;
+  b->ntiles = t.knn ? (int)(t.N + 1) : (int)t.tiles.size();
   const size_t need = batch_layout(b, m, nullptr, b->ntiles);
   char* base = (char*)d_ws;
   if (!base) {
@@ -523,7 +579,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
      // Only for a short partial round (<= 1/4 of the CUs): 64x40 (32 of 256 tiles) gains 6% per step;
      // at 256x40 (128 of 256) the split grid lost 0.8% (profiles/r2/split_*)
     const long tiles1 = (t.E + kTileRows - 1) / kTileRows * (H / 256);
-    if (m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu && (tiles1 % m->ncu) * 4 <= m->ncu) {
+    if (!t.knn && m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu && (tiles1 % m->ncu) * 4 <= m->ncu) {
       long full = tiles1 / m->ncu * m->ncu;
       full -= full % (H / 256);
       const long rows_a = full / (H / 256) * kTileRows;
@@ -544,11 +600,17 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   up(b->node_off, t.noff.data(), (B + 1) * sizeof(int));
   up(b->edge_off, t.eoff.data(), (B + 1) * sizeof(long));
   up(b->n2g, t.n2g.data(), t.N * sizeof(int));
-  up(b->ei, t.ei.data(), t.E * sizeof(int));
-  up(b->ej, t.ej.data(), t.E * sizeof(int));
-  up(b->node_estart, t.estart.data(), t.N * sizeof(long));
-  up(b->node_n, t.nn.data(), t.N * sizeof(int));
-  up(b->tiles, t.tiles.data(), t.tiles.size() * sizeof(int2));
+  if (t.knn) {
+    up(b->cand_off, t.coff.data(), (B + 1) * sizeof(long));
+    b->E = 0;  // no graph yet
+    b->ntiles = 0;
+  } else {
+    up(b->ei, t.ei.data(), t.E * sizeof(int));
+    up(b->ej, t.ej.data(), t.E * sizeof(int));
+    up(b->node_estart, t.estart.data(), t.N * sizeof(long));
+    up(b->node_n, t.nn.data(), t.N * sizeof(int));
+    up(b->tiles, t.tiles.data(), t.tiles.size() * sizeof(int2));
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     chm_batch_destroy(b);
@@ -562,13 +624,16 @@ extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int
   return batch_build(m, h_natoms, B, max_pairs, nullptr, 0, nullptr, out);
 }
 
-extern "C" size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs) {
+extern "C" size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs,
+                                               const chm_batch_options* opts) {
   if (!m || !h_natoms || B < 1 || max_pairs < 1 || max_pairs > 2) {
     fail(CHM_E_ARG, "bad batch arguments");
     return 0;
   }
+  BatchOpts bo;
+  if (batch_opts(opts, bo)) return 0;
   BatchTables t;
-  if (batch_tables(h_natoms, B, t)) return 0;
+  if (batch_tables(h_natoms, B, t, bo)) return 0;
   chm_batch b;
   b.m = m;
   b.math = m->math;
@@ -576,7 +641,22 @@ extern "C" size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h
   b.P = max_pairs;
   b.N = t.N;
   b.E = t.E;
+  b.knn = bo.knn;
+  b.C_cap = t.C;
   return batch_layout(&b, m, nullptr, count_tiles(t));
+}
+
+extern "C" size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs) {
+  return chm_batch_workspace_bytes_ex(m, h_natoms, B, max_pairs, nullptr);
+}
+
+extern "C" int chm_batch_create_ex(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs,
+                                   const chm_batch_options* opts, void* d_workspace, size_t workspace_bytes,
+                                   void* stream, chm_batch** out) {
+  BatchOpts bo;
+  const int rc = batch_opts(opts, bo);
+  if (rc) return rc;
+  return batch_build(m, h_natoms, B, max_pairs, d_workspace, workspace_bytes, (hipStream_t)stream, out, bo);
 }
 
 extern "C" int chm_batch_create_with_workspace(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs,
@@ -719,12 +799,63 @@ static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which
 }
 
 // heads: bit 0 = node heads (types + coords), bit 1 = lattice head
+// knn batches: the radius graph of these coordinates (knn.hip), edges grouped by source node. One
+// stream sync reads the out-degrees back to size the launches and build the segment tiles.
+static int knn_build(chm_batch* b, const float* x, const float* lat, hipStream_t s) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+    return fail(CHM_E_UNSUPPORTED, "knn batches rebuild their edges on the host's schedule: no graph capture");
+  const int B = b->B;
+  const long N = b->N;
+  KnnArgs k;
+  std::memset(&k, 0, sizeof(k));
+  k.x = x; k.lat = lat; k.natoms = b->natoms; k.node_off = b->node_off; k.cand_off = b->cand_off;
+  k.cand_key = b->cand_key; k.cand_d2 = b->cand_d2; k.cand2 = b->cand2; k.atom_cnt = b->atom_cnt;
+  k.max_nb = b->knn_max_nb; k.fin_key = b->fin_key; k.fin_fd = b->fin_fd; k.deg = b->deg; k.cryst_fin = b->cryst_fin;
+  k.node_estart = b->node_estart; k.ei = b->ei; k.ej = b->ej; k.fd = b->fd;
+  HIPCHK(knn_candidates(k, B, s));
+  b->h_deg.resize(N);
+  HIPCHK(hipMemcpyAsync(b->h_deg.data(), b->deg, N * sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  b->h_estart.resize(N);
+  b->h_tiles.clear();
+  long E = 0, rows = 0;
+  int cur0 = 0;
+  for (long v = 0; v < N; ++v) {  // segment tiles: runs of whole nodes of <= 256 edge rows (as batch_fill)
+    const int d = b->h_deg[v];
+    if (d > kTileRows) return fail(CHM_E_UNSUPPORTED, "knn: a node with more than 256 edges");
+    b->h_estart[v] = E;
+    E += d;
+    if (rows + d > kTileRows) {
+      b->h_tiles.push_back(make_int2(cur0, (int)v));
+      cur0 = (int)v;
+      rows = 0;
+    }
+    rows += d;
+  }
+  b->h_tiles.push_back(make_int2(cur0, (int)N));
+  if (E > b->E_cap)
+    return fail(CHM_E_UNSUPPORTED, "knn: the graph has " + std::to_string(E) + " edges, above the batch capacity " +
+                                       std::to_string(b->E_cap) + " (chm_batch_options.knn_edges_per_atom)");
+  HIPCHK(hipMemcpyAsync(b->node_estart, b->h_estart.data(), N * sizeof(long), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b->node_n, b->h_deg.data(), N * sizeof(int), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b->tiles, b->h_tiles.data(), b->h_tiles.size() * sizeof(int2), hipMemcpyHostToDevice, s));
+  HIPCHK(knn_place(k, B, s));
+  b->E = E;
+  b->ntiles = (int)b->h_tiles.size();
+  return CHM_OK;
+}
+
 // reuse_cond: the FiLM conditioning (cond_in + the conditioning MLP) of the previous call on this batch
 // is still valid (same t and text: the corrector call of a reverse step, chemeleon.py:438-448)
 static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, const float* lat, const float* temb,
                        int tstride, const int* d_t, const float* text0, const float* text1, int heads,
                        hipStream_t s, bool reuse_cond = false) {
   const chm_model* m = b->m;
+  if (b->knn) {
+    const int rc = knn_build(b, x, lat, s);
+    if (rc) return rc;
+  }
   const int L = m->d.num_layers, X = m->d.text_dim, B = b->B;
   const long N = b->N, E = b->E, R = (long)P * N;
   const int CIN = TD + X;
@@ -741,7 +872,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   }
   HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H)));
   if (b->math == MATH_SPLIT16)
-    HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s));  // fp16 hi/lo planes [2][E][768] in F's bytes
+    HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s, b->knn ? b->fd : nullptr));  // fp16 hi/lo split rows
   else
     HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
   for (int l0 = 0; l0 < L; l0 += kGBLayers) {  // all layers' per-graph terms, one launch per 16 layers
@@ -767,7 +898,9 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       g.amax = rmx(RMX_HL);
       HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s, w.WAB16, w.WABsc));
     }
-    if (b->math == MATH_SPLIT16) {
+    if (b->math == MATH_SPLIT16 && E == 0) {  // (knn: no atom within any other's radius: every mean is 0)
+      HIPCHK(hipMemsetAsync(b->agg, 0, (size_t)P * N * H * sizeof(float), s));
+    } else if (b->math == MATH_SPLIT16) {
       // split16: fp16 hi/lo split rows throughout (edge_gemm.hip). S lives in S's bytes as
       // split rows [P*E][H/32][2][32] plus one packed exponent word per row (rowmax buffer).
       int* sexp = reinterpret_cast<int*>(b->rowmax);
@@ -975,8 +1108,24 @@ extern "C" int chm_edge_features(chm_batch* b, const float* x, float* feat, void
   return CHM_OK;
 }
 
+extern "C" int chm_knn_edges(chm_batch* b, const float* x, const float* lat, int32_t* src, int32_t* dst, float* fd,
+                             int64_t capacity, int64_t* n_edges, void* stream) {
+  if (!b || !x || !lat || !n_edges) return fail(CHM_E_ARG, "NULL argument");
+  if (!b->knn) return fail(CHM_E_ARG, "not a knn batch");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = knn_build(b, x, lat, s);
+  if (rc) return rc;
+  *n_edges = b->E;
+  if (b->E > capacity) return CHM_OK;
+  if (src) HIPCHK(hipMemcpyAsync(src, b->ei, b->E * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (dst) HIPCHK(hipMemcpyAsync(dst, b->ej, b->E * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (fd) HIPCHK(hipMemcpyAsync(fd, b->fd, b->E * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return CHM_OK;
+}
+
 extern "C" int chm_edge_features_split(chm_batch* b, const float* x, void* split, void* stream) {
   if (!b || !x || !split) return fail(CHM_E_ARG, "NULL argument");
-  HIPCHK(fourier_h(x, b->ei, b->ej, b->E, split, (hipStream_t)stream));
+  // (knn batches: the features of the graph built by the last decoder call / chm_knn_edges)
+  HIPCHK(fourier_h(x, b->ei, b->ej, b->E, split, (hipStream_t)stream, b->knn ? b->fd : nullptr));
   return CHM_OK;
 }

@@ -250,8 +250,11 @@ class Chemeleon(nn.Module):
             raise ValueError("natoms and texts must have the same number of elements.")
         if noise not in ("torch", "philox"):
             raise ValueError("noise must be 'torch' or 'philox'")
-        if graph is None:
-            graph = noise == "philox"
+        knn = getattr(self.decoder, "edge_style", "fc") == "knn"
+        if graph is None:  # knn edges are rebuilt from the coordinates with a host sync: eager only
+            graph = noise == "philox" and not knn
+        if graph and knn:
+            raise ValueError("edge_style='knn' rebuilds its edges every decoder call and cannot run as a captured graph")
         dev = self.device
         if dev.type != "cuda":
             raise RuntimeError("Chemeleon (chemeleon_amd) samples on a HIP device only; call .to('cuda') first")

@@ -108,21 +108,24 @@ class HipBatch:
     budgeted with the rest of the process's device tensors. A batch is scratch for one stream:
     CSPNet.hip_batch keys its cache by stream."""
 
-    def __init__(self, model: _HipModel, natoms, max_pairs: int):
+    def __init__(self, model: _HipModel, natoms, max_pairs: int, knn: bool = False, max_neighbors: int = 20,
+                 knn_edges_per_atom: int = 128):
         L = _lib.load()
         nat = [int(n) for n in natoms]
         arr = (ctypes.c_int32 * len(nat))(*nat)
-        need = int(L.chm_batch_workspace_bytes(model.handle, arr, len(nat), max_pairs))
+        opts = _lib.chm_batch_options(_lib.EDGES_KNN if knn else _lib.EDGES_FC, int(max_neighbors),
+                                      int(knn_edges_per_atom), 0)
+        need = int(L.chm_batch_workspace_bytes_ex(model.handle, arr, len(nat), max_pairs, ctypes.byref(opts)))
         if need == 0:
-            _lib.check(-1, "chm_batch_workspace_bytes")
+            _lib.check(-1, "chm_batch_workspace_bytes_ex")
         h = _lib.c_void_p()
         with torch.cuda.device(model.device):
             # 256-byte alignment: the caching allocator returns 512-byte aligned blocks
             self.workspace = torch.empty(need, dtype=torch.uint8, device=model.device)
-            _lib.check(L.chm_batch_create_with_workspace(model.handle, arr, len(nat), max_pairs,
-                                                         _lib.ptr(self.workspace), need,
-                                                         _lib.stream_handle(model.device), h),
-                       "chm_batch_create_with_workspace")
+            _lib.check(L.chm_batch_create_ex(model.handle, arr, len(nat), max_pairs, ctypes.byref(opts),
+                                             _lib.ptr(self.workspace), need, _lib.stream_handle(model.device), h),
+                       "chm_batch_create_ex")
+        self.knn = bool(knn)
         self.handle = h
         self.model = model  # keep the weights alive
         self.natoms = tuple(nat)
@@ -181,8 +184,8 @@ class CSPNet(nn.Module):
 
     def _check_supported(self):
         why = []
-        if self.edge_style != "fc":
-            why.append("edge_style='knn' (the reference's knn path raises NameError: data_utils.py:7,307)")
+        if self.edge_style not in ("fc", "knn"):
+            why.append(f"edge_style={self.edge_style!r}")
         if self.smooth:
             why.append("smooth=True")
         if not self.ln or not self.ip:
@@ -239,8 +242,9 @@ class CSPNet(nn.Module):
         fresh, uncached batch (one per concurrent lane of a captured step)."""
         m = self.hip_model()
         nat = tuple(int(n) for n in natoms)
+        knn = dict(knn=self.edge_style == "knn", max_neighbors=self.max_neighbors)
         if private:
-            return HipBatch(m, nat, max_pairs)
+            return HipBatch(m, nat, max_pairs, **knn)
         if stream is None:
             stream = torch.cuda.current_stream(m.device)
         key = (nat, max_pairs, int(stream.cuda_stream))
@@ -250,7 +254,7 @@ class CSPNet(nn.Module):
                 if len(self._batches) >= 4:
                     self._batches.pop(next(iter(self._batches)))
                 with torch.cuda.stream(stream):
-                    b = HipBatch(m, nat, max_pairs)
+                    b = HipBatch(m, nat, max_pairs, **knn)
                 self._batches[key] = b
             return b
 

@@ -128,6 +128,35 @@ size_t chm_batch_workspace_bytes(const chm_model* m, const int32_t* h_natoms, in
 int chm_batch_create_with_workspace(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs,
                                     void* d_workspace, size_t workspace_bytes, void* stream, chm_batch** out);
 
+/* Edge styles (CSPNet(edge_style=...), cspnet.py:319-343). CHM_EDGES_KNN is the reference's radius
+ * graph (radius_graph_pbc + neighbour cap + symmetric reorder, data_utils.py:151-398,
+ * cspnet.py:236-343; the reference needs torch_scatter's segment ops for it). Its edges depend on the
+ * coordinates, so every decoder call of a knn batch rebuilds them on the device and synchronises
+ * `stream` once to size the launches: knn batches cannot be captured into a graph. split16
+ * arithmetic only. */
+#define CHM_EDGES_FC 0
+#define CHM_EDGES_KNN 1
+typedef struct chm_batch_options {
+  int32_t edge_style;          /* CHM_EDGES_FC (default) or CHM_EDGES_KNN */
+  int32_t max_neighbors;       /* knn: max_num_neighbors_threshold (CSPNet max_neighbors, default 20) */
+  int32_t knn_edges_per_atom;  /* knn: edge capacity per atom after symmetrisation (default 128); a
+                                  decoder call whose graph has more edges fails with CHM_E_UNSUPPORTED */
+  int32_t reserved;
+} chm_batch_options;
+/* chm_batch_workspace_bytes / chm_batch_create_with_workspace with options (NULL = fc defaults);
+ * d_workspace NULL: the library allocates (as chm_batch_create). */
+size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs,
+                                    const chm_batch_options* opts);
+int chm_batch_create_ex(const chm_model* m, const int32_t* h_natoms, int num_graphs, int max_pairs,
+                        const chm_batch_options* opts, void* d_workspace, size_t workspace_bytes, void* stream,
+                        chm_batch** out);
+/* knn batches: build the edge list of these coordinates now (as a decoder call does) and copy it out,
+ * grouped by source node in the reference's order within each node: d_src / d_dst [capacity] int32
+ * global node indices, d_frac_diff [capacity, 3]; *n_edges = the edge count (nothing is copied when it
+ * exceeds capacity). Any of the output pointers may be NULL. */
+int chm_knn_edges(chm_batch* b, const float* d_frac, const float* d_lattices, int32_t* d_src, int32_t* d_dst,
+                  float* d_frac_diff, int64_t capacity, int64_t* n_edges, void* stream);
+
 /* One decoder call for `pairs` conditionings that share atom types,
  * coordinates and lattices (pairs = 1: CSPNet.forward, cspnet.py:345-405;
  * pairs = 2: the two calls of Chemeleon.model_predictions, chemeleon.py:258-285).
