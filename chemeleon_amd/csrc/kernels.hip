@@ -369,7 +369,7 @@ __device__ __forceinline__ void ln512(f32x4& v0, f32x4& v1, const float* w, cons
 }
 
 // FiLM (cspnet.py:78-97) fused with the next CSPLayer's LayerNorm (:175-176):
-// Hres = SiLU(LN_f(Y) * scale_g + shift_g) + Hres ; Hl = LN_l(Hres)
+// Hres = SiLU(LN_f(Y) * scale_g + shift_g) + Hres ; Hl = LN_l(Hres)   (Y null, no FilmLayer: Hl = LN_l(Hres))
 __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, float* __restrict__ Hres,
                                                  float* __restrict__ Hl, const float* __restrict__ cond_emb,
                                                  const int* __restrict__ n2g, long N, int B, int P,
@@ -378,22 +378,29 @@ __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, fl
   const int lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N * P) return;
-  const long c = r / N, i = r - c * N;
-  const long crow = c * B + n2g[i];
-  const f32x4* y4 = reinterpret_cast<const f32x4*>(Y + r * H);
-  f32x4 v0 = y4[lane], v1 = y4[64 + lane];
-  ln512(v0, v1, fw, fb, lane);
-  const f32x4* sc = reinterpret_cast<const f32x4*>(cond_emb + crow * 2 * H);
-  const f32x4* sh = reinterpret_cast<const f32x4*>(cond_emb + crow * 2 * H + H);
-  v0 = v0 * sc[lane] + sh[lane];
-  v1 = v1 * sc[64 + lane] + sh[64 + lane];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { v0[k] = silu(v0[k]); v1[k] = silu(v1[k]); }
   f32x4* h4 = reinterpret_cast<f32x4*>(Hres + r * H);
-  v0 += h4[lane];
-  v1 += h4[64 + lane];
-  h4[lane] = v0;
-  h4[64 + lane] = v1;
+  f32x4 v0, v1;
+  if (Y) {
+    const long c = r / N, i = r - c * N;
+    const long crow = c * B + n2g[i];
+    const f32x4* y4 = reinterpret_cast<const f32x4*>(Y + r * H);
+    v0 = y4[lane];
+    v1 = y4[64 + lane];
+    ln512(v0, v1, fw, fb, lane);
+    const f32x4* sc = reinterpret_cast<const f32x4*>(cond_emb + crow * 2 * H);
+    const f32x4* sh = reinterpret_cast<const f32x4*>(cond_emb + crow * 2 * H + H);
+    v0 = v0 * sc[lane] + sh[lane];
+    v1 = v1 * sc[64 + lane] + sh[64 + lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v0[k] = silu(v0[k]); v1[k] = silu(v1[k]); }
+    v0 += h4[lane];
+    v1 += h4[64 + lane];
+    h4[lane] = v0;
+    h4[64 + lane] = v1;
+  } else {  // (no FilmLayer: Hres passes through)
+    v0 = h4[lane];
+    v1 = h4[64 + lane];
+  }
   ln512(v0, v1, lw, lb, lane);
   f32x4* l4 = reinterpret_cast<f32x4*>(Hl + r * H);
   l4[lane] = v0;

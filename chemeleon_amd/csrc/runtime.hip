@@ -67,6 +67,7 @@ struct chm_model {
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int ncu = 0;           // compute units of the device the model lives on
+  int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
   std::vector<LayerW> layers;
@@ -112,13 +113,16 @@ struct chm_batch {
 extern "C" const char* chm_last_error(void) { return g_err.c_str(); }
 extern "C" const char* chm_version(void) { return "chemeleon-mi355x 0.3 (gfx950; split16 / bf16x3 / f32 MFMA)"; }
 
-extern "C" int chm_num_params(const chm_dims* d) { return d ? 7 + 10 * d->num_layers + 6 : 0; }
+// (time_dim = text_dim = 0: a CSPNet without FilmLayer, cspnet.py:210-211, e.g. CrystalClip's graph encoder)
+static bool film_less(const chm_dims* d) { return d->time_dim == 0 && d->text_dim == 0; }
+extern "C" int chm_num_params(const chm_dims* d) { return d ? (film_less(d) ? 1 : 7) + 10 * d->num_layers + 6 : 0; }
 
 static int check_dims(const chm_dims* d) {
   if (!d) return fail(CHM_E_ARG, "dims is NULL");
   if (d->hidden_dim != H) return fail(CHM_E_UNSUPPORTED, "hidden_dim must be 512 in this build");
   if (d->num_freqs != NF) return fail(CHM_E_UNSUPPORTED, "num_freqs must be 128 in this build");
-  if (d->time_dim != TD) return fail(CHM_E_UNSUPPORTED, "time_dim must be 128 in this build");
+  if (d->time_dim != TD && !film_less(d))
+    return fail(CHM_E_UNSUPPORTED, "time_dim must be 128 in this build (or time_dim = text_dim = 0)");
   if (d->text_dim < 0 || (TD + d->text_dim) % 16) return fail(CHM_E_UNSUPPORTED, "time_dim + text_dim must be a multiple of 16");
   if (d->max_atoms < 1 || d->max_atoms + 3 > HEADS_N) return fail(CHM_E_UNSUPPORTED, "max_atoms must be in [1, 125]");
   if (d->num_layers < 1 || d->num_layers > 64) return fail(CHM_E_ARG, "num_layers out of range");
@@ -136,7 +140,9 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (!p[i]) return fail(CHM_E_ARG, "parameter pointer " + std::to_string(i) + " is NULL");
   hipStream_t s = (hipStream_t)stream;
   const int A = dims->max_atoms, L = dims->num_layers, X = dims->text_dim;
-  const int CIN = TD + X, W1K = 2 * H + 9 + FD;
+  const bool film = !film_less(dims);
+  const int CIN = film ? TD + X : 0, W1K = 2 * H + 9 + FD;
+  const int PL = film ? 7 : 1;  // first layer parameter
   {
     hipError_t e0 = gemm_init();
     if (e0 == hipSuccess) e0 = edge_gemm_init();
@@ -170,6 +176,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
 
   chm_model* m = new chm_model();
   m->d = *dims;
+  m->film = film;
   m->mem_floats = off;
   hipError_t e = hipMalloc(&m->mem, off * sizeof(float));
   if (e != hipSuccess) {
@@ -196,14 +203,16 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   } while (0)
   CK(hipMemsetAsync(base, 0, off * sizeof(float), s));
   CK(cp(o_emb, p[0], (size_t)A * H));
-  CK(cp(o_Wc, p[1], (size_t)2 * H * CIN));
-  CK(cp(o_bc, p[2], 2 * H));
-  CK(cp(o_Wp, p[3], H * H));
-  CK(cp(o_bp, p[4], H));
-  CK(cp(o_fw, p[5], H));
-  CK(cp(o_fb, p[6], H));
+  if (film) {  // (film-less: the FiLM arena stays zero and is never read)
+    CK(cp(o_Wc, p[1], (size_t)2 * H * CIN));
+    CK(cp(o_bc, p[2], 2 * H));
+    CK(cp(o_Wp, p[3], H * H));
+    CK(cp(o_bp, p[4], H));
+    CK(cp(o_fw, p[5], H));
+    CK(cp(o_fb, p[6], H));
+  }
   for (int l = 0; l < L; ++l) {
-    const float* const* q = p + 7 + 10 * l;
+    const float* const* q = p + PL + 10 * l;
     // edge_mlp.0.weight [H][2H+9+FD] -> WAB = [W1[:, 0:H] ; W1[:, H:2H]], Wcl = W1[:, 2H:2H+9], D = W1[:, 2H+9:]
     CK(cp2(lo[l * 12 + 0], H, q[0], W1K, 0, H, H));
     CK(cp2(lo[l * 12 + 0] + (size_t)H * H, H, q[0], W1K, H, H, H));
@@ -219,7 +228,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     CK(cp(lo[l * 12 + 10], q[8], H));
     CK(cp(lo[l * 12 + 11], q[9], H));
   }
-  const float* const* hq = p + 7 + 10 * L;  // coord_out.w, lattice_out.w, type_out.w, type_out.b, final_ln.w, final_ln.b
+  const float* const* hq = p + PL + 10 * L;  // coord_out.w, lattice_out.w, type_out.w, type_out.b, final_ln.w, final_ln.b
   CK(cp(o_Wh, hq[2], (size_t)A * H));                 // rows 0..A-1: type_out
   CK(cp(o_Wh + (size_t)A * H, hq[0], (size_t)3 * H)); // rows A..A+2: coord_out
   CK(cp(o_bh, hq[3], A));
@@ -285,7 +294,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     char* p3 = (char*)m->mem3;
     for (auto& j : jobs) {
       *j.dst = p3;
-      hipError_t e3 = split_planes(j.src, (long)j.n, p3, s);
+      hipError_t e3 = j.n ? split_planes(j.src, (long)j.n, p3, s) : hipSuccess;  // (film-less: no Wc)
       if (e3 != hipSuccess) {
         (void)hipFree(m->mem); (void)hipFree(m->mem3);
         delete m;
@@ -864,7 +873,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   const bool n16 = b->math == MATH_SPLIT16 && m->node16 && m->node_glds;
   const long RS = (long)b->P * N;
   auto rmx = [&](int k) { return n16 ? b->rmx + k * RS : nullptr; };
-  if (!reuse_cond) {
+  if (m->film && !reuse_cond) {
     HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
@@ -886,12 +895,14 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
-    {  // FiLM projection (cspnet.py:92)
+    if (m->film) {  // FiLM projection (cspnet.py:92)
       GemmArgs g = gargs(R, H, H, b->Hres, H, m->Wp, b->Y, H);
       g.bias = m->bp; g.amax = rmx(RMX_H);
       HIPCHK(run_gemm(b, g, EPI_STD, m->Wp3, s, m->Wp16, m->Wpsc));
     }
-    HIPCHK(film_ln(b->Y, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s, rmx(0), RS));
+    // FiLM + residual + the layer's LayerNorm (film-less: the LayerNorm only)
+    HIPCHK(film_ln(m->film ? b->Y : nullptr, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s,
+                   rmx(0), RS));
     {  // per-node halves of the first edge layer: [P | Q] = Hl [A ; Bm]^T, P += b1 + C vec(LL^T)
       GemmArgs g = gargs(R, 2 * H, H, b->Hl, H, w.WAB, b->PQ, 2 * H);
       g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
@@ -1002,7 +1013,7 @@ extern "C" int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* a, co
                                    float* lattice_out, float* coords_out, float* node_out, void* stream) {
   if (!b) return fail(CHM_E_ARG, "batch is NULL");
   if (pairs < 1 || pairs > b->P) return fail(CHM_E_ARG, "pairs must be in [1, max_pairs]");
-  if (!a || !x || !lat || !temb) return fail(CHM_E_ARG, "inputs must not be NULL");
+  if (!a || !x || !lat || (b->m->film && !temb)) return fail(CHM_E_ARG, "inputs must not be NULL");
   const int X = b->m->d.text_dim;
   if (X > 0 && !text) return fail(CHM_E_ARG, "text embeddings required (text_dim > 0)");
   hipStream_t s = (hipStream_t)stream;
@@ -1025,6 +1036,7 @@ static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, fl
                        int64_t graph_base, hipStream_t s) {
   if (!b || !sc) return fail(CHM_E_ARG, "batch / schedule is NULL");
   if (b->P < 2) return fail(CHM_E_ARG, "sampling needs a batch created with max_pairs = 2");
+  if (!b->m->film) return fail(CHM_E_ARG, "sampling needs a time-conditioned decoder (time_dim > 0)");
   if (!d_t && (t < 1 || t > sc->T)) return fail(CHM_E_ARG, "t out of range");
   if (!d_a || !d_x || !d_l || !sc->d_coef || !sc->d_time_emb || !sc->d_q_one_step || !sc->d_q_mats)
     return fail(CHM_E_ARG, "NULL state or schedule table");

@@ -260,7 +260,8 @@ class CSPNet(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def _run(self, pairs, atom_types, frac_coords, lattices, num_atoms, t, text, need_nodes=True):
-        if t is None:
+        film = self.time_dim > 0 or self.text_dim > 0
+        if t is None and film:
             raise NotImplementedError("time embeddings are required (the sampling path always passes them)")
         natoms = num_atoms.tolist() if torch.is_tensor(num_atoms) else list(num_atoms)
         b = self.hip_batch(natoms, max_pairs=max(pairs, 1))
@@ -268,11 +269,11 @@ class CSPNet(nn.Module):
         a = atom_types.long().contiguous()
         x = frac_coords.float().contiguous()
         lat = lattices.float().contiguous()
-        te = t.float().contiguous()
-        tx = text.float().contiguous() if text is not None else None
+        te = t.float().contiguous() if film else None  # (no FilmLayer: time and text are not used)
+        tx = text.float().contiguous() if text is not None and film else None
         _lib.require_device(a, x, lat, te, tx)
         B, N = b.num_graphs, b.num_nodes
-        if a.shape[0] != N or x.shape != (N, 3) or lat.shape != (B, 3, 3) or te.shape != (B, self.time_dim):
+        if a.shape[0] != N or x.shape != (N, 3) or lat.shape != (B, 3, 3) or (film and te.shape != (B, self.time_dim)):
             raise ValueError("decoder input shapes do not match num_atoms")
         if self.text_dim > 0 and (tx is None or tx.shape[-1] != self.text_dim):
             raise ValueError("text embeddings of width text_dim are required")

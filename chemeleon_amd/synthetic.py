@@ -96,6 +96,22 @@ def synthetic_state_dict(cfg: Dict, seed: int = 0) -> "OrderedDict[str, torch.Te
     )
 
 
+def synthetic_clip_graph_state_dict(cfg: Dict, clip_dim: int, seed: int = 0) -> "OrderedDict[str, torch.Tensor]":
+    """Graph side of the reference CrystalClip (crystal_clip.py:34-73): `graph_encoder.*` (a CSPNet
+    with time_dim = text_dim = 0, same recipe per key) and `graph_proj.{0,1,3}.*` (Linear, LayerNorm,
+    GELU, Linear to clip_dim)."""
+    c = dict(cfg)
+    c["time_dim"] = 0
+    c["text_dim"] = 0
+    sd = OrderedDict(("graph_encoder." + k, synthetic_tensor(k, shape, seed)) for k, shape in cspnet_param_shapes(c).items())
+    H = cfg["hidden_dim"]
+    for k, shape in (("graph_proj.0.weight", (H, H)), ("graph_proj.0.bias", (H,)), ("graph_proj.1.weight", (H,)),
+                     ("graph_proj.1.bias", (H,)), ("graph_proj.3.weight", (clip_dim, H)), ("graph_proj.3.bias", (clip_dim,))):
+        kk = k.replace("graph_proj.1", "graph_proj.norm")  # (LayerNorm recipe for index 1)
+        sd[k] = synthetic_tensor(kk, shape, seed)
+    return sd
+
+
 def weights_crc(sd) -> int:
     """CRC32 over the tensors of a state dict in key order; stored in every
     fixture so a changed recipe is detected instead of silently compared."""

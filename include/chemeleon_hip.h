@@ -37,9 +37,10 @@ extern "C" {
 
 /* Hyper-parameters of the score network; mirrors the CSPNet constructor
  * (chemeleon/modules/cspnet.py:185-202). This build implements
- * hidden_dim = 512, num_freqs = 128, edge_style "fc", ln = ip = 1,
- * smooth = 0, act "silu", dis_emb "sin"; other values return
- * CHM_E_UNSUPPORTED from chm_model_create. */
+ * hidden_dim = 512, num_freqs = 128, time_dim = 128 (or time_dim = text_dim = 0:
+ * no FilmLayer), ln = ip = 1, smooth = 0, act "silu", dis_emb "sin"; other values
+ * return CHM_E_UNSUPPORTED from chm_model_create. The edge style ("fc" or
+ * "knn") is a property of the batch (chm_batch_options). */
 typedef struct {
   int hidden_dim;  /* 512 */
   int time_dim;    /* 128 */
@@ -67,7 +68,8 @@ int chm_num_params(const chm_dims* dims);
  * d_params[i] points to the i-th state_dict tensor in this order (row-major,
  * contiguous, fp32, nn.Linear layout [out][in]):
  *   node_embedding.weight, film_layer.mlp_cond.0.{weight,bias},
- *   film_layer.proj.{weight,bias}, film_layer.norm.{weight,bias},
+ *   film_layer.proj.{weight,bias}, film_layer.norm.{weight,bias} (not when
+ *   time_dim = text_dim = 0),
  *   for l in 0..L-1: csp_layer_l.{edge_mlp.0.weight, edge_mlp.0.bias,
  *     edge_mlp.2.weight, edge_mlp.2.bias, node_mlp.0.weight, node_mlp.0.bias,
  *     node_mlp.2.weight, node_mlp.2.bias, layer_norm.weight, layer_norm.bias},
@@ -166,6 +168,9 @@ int chm_knn_edges(chm_batch* b, const float* d_frac, const float* d_lattices, in
  * Outputs (any may be NULL to skip it):
  *   d_types_out [pairs,N,A], d_lattice_out [pairs,B,3,3], d_coords_out [pairs,N,3],
  *   d_node_out  [pairs,N,H] (final-LayerNorm node features). */
+/* (A model created with time_dim = text_dim = 0 has no FilmLayer, cspnet.py:210-211: the reference's
+ * CrystalClip graph encoder. Its parameter list omits the six film_layer.* tensors, d_time_emb may be
+ * NULL, and it cannot sample.) */
 int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* d_atom_types, const float* d_frac,
                         const float* d_lattices, const float* d_time_emb, int time_stride, const float* d_text,
                         float* d_types_out, float* d_lattice_out, float* d_coords_out, float* d_node_out,

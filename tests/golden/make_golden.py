@@ -448,6 +448,49 @@ def gen_knn(chm, csp):
     save("knn.npz", **rec)
 
 
+CLIP_DIM = 256
+
+
+def clip_graph_config(edge_style):
+    c = default_config()
+    c.update({"edge_style": edge_style, "clip_dim": CLIP_DIM, "graph_pooling": "mean"})
+    return c
+
+
+def gen_clip_graph(chm, csp):
+    """CrystalClip.get_graph_embeds (crystal_clip.py:98-112) with the reference's own modules: the
+    time- and text-free CSPNet graph encoder (:34-52; fc, and knn with the segment ops injected),
+    the reference scatter_mean pooling and the graph_proj head (:67-72), synthetic weights. (The
+    reference CrystalClip itself builds a BERT from the hub in its constructor, which cannot run
+    offline; these are the lines of get_graph_embeds on its modules.)"""
+    from chemeleon_amd.synthetic import synthetic_clip_graph_state_dict
+    import chemeleon.utils.scatter as sc
+    _inject_segment_ops()
+    rec = {}
+    for edge_style, cases in (("fc", (("fc4x6", [6, 6, 6, 6], 41), ("fcragged", [3, 5, 8, 1, 12], 42))),
+                              ("knn", (("knnsmall", [3, 5, 8, 1, 12], 31),))):
+        cfg = clip_graph_config(edge_style)
+        sd = synthetic_clip_graph_state_dict(cfg, CLIP_DIM)
+        enc = csp.CSPNet(hidden_dim=512, time_dim=0, text_dim=0, num_layers=6, max_atoms=104, act_fn="silu",
+                         dis_emb="sin", num_freqs=128, edge_style=edge_style, cutoff=6.0, max_neighbors=20, ln=True,
+                         ip=True, smooth=False, pred_atom_types=True)
+        enc.load_state_dict({k[len("graph_encoder."):]: v for k, v in sd.items() if k.startswith("graph_encoder.")})
+        proj = nn.Sequential(nn.Linear(512, 512), nn.LayerNorm(512), nn.GELU(), nn.Linear(512, CLIP_DIM))
+        proj.load_state_dict({k[len("graph_proj."):]: v for k, v in sd.items() if k.startswith("graph_proj.")})
+        rec[f"{edge_style}_weights_crc"] = weights_crc(sd)
+        for tag, natoms, seed in cases:
+            a, x, lat = knn_crystals(natoms, seed, 4.0, 7.0)
+            nat = torch.tensor(natoms)
+            n2g = torch.arange(len(natoms)).repeat_interleave(nat)
+            with torch.no_grad():
+                o = enc(t=None, atom_types=a, frac_coords=x, lattices=lat, num_atoms=nat, node2graph=n2g)
+                pooled = sc.scatter_mean(o.node_features, n2g, dim=0)
+                emb = proj(pooled)
+            rec.update({f"{tag}_natoms": nat, f"{tag}_atom_types": a, f"{tag}_frac": x, f"{tag}_lattices": lat,
+                        f"{tag}_node_features": o.node_features, f"{tag}_pooled": pooled, f"{tag}_embeds": emb})
+    save("clip_graph.npz", **rec)
+
+
 def _run_reference_trajectory(m, T, every):
     from chemeleon.modules import schema
     states = []
@@ -601,5 +644,7 @@ if __name__ == "__main__":
         gen_text(chm, csp)
     if "knn" in which:
         gen_knn(chm, csp)
+    if "clip_graph" in which:
+        gen_clip_graph(chm, csp)
     if "trajectory1000" in which:
         gen_trajectory(chm, csp, T=1000, every=10)
