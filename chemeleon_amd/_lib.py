@@ -37,6 +37,12 @@ class chm_batch_options(ctypes.Structure):
 EDGES_FC, EDGES_KNN = 0, 1
 
 
+class chm_train_tables(ctypes.Structure):
+    _fields_ = [("T", c_int), ("d_coef4", c_void_p), ("d_q_one_step", c_void_p), ("d_q_mats", c_void_p),
+                ("hybrid_coeff", c_float), ("cost_atom_types", c_float), ("cost_lattice", c_float),
+                ("cost_coords", c_float)]
+
+
 class chm_schedule(ctypes.Structure):
     _fields_ = [("T", c_int), ("d_coef", c_void_p), ("d_time_emb", c_void_p), ("d_q_one_step", c_void_p),
                 ("d_q_mats", c_void_p)]
@@ -63,6 +69,7 @@ SIGNATURES = {
     "chm_batch_create_ex": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_int, c_int,
                                     ctypes.POINTER(chm_batch_options), c_void_p, ctypes.c_size_t, c_void_p,
                                     ctypes.POINTER(c_void_p)]),
+    "chm_training_loss": (c_int, [c_void_p, ctypes.POINTER(chm_train_tables)] + [c_void_p] * 17),
     "chm_knn_edges": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
                               ctypes.POINTER(c_i64), c_void_p]),
     "chm_debug_philox": (c_int, [c_u64, c_int, c_int, c_i64, c_i64, c_int, c_void_p, c_void_p]),

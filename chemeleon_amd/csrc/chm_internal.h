@@ -90,6 +90,23 @@ struct KnnArgs {
 };
 hipError_t knn_candidates(const KnnArgs& g, int B, hipStream_t s);  // pairs, cap, symmetric list, degrees
 hipError_t knn_place(const KnnArgs& g, int B, hipStream_t s);       // grouped by source (node_estart set)
+// training forward / validation loss (kernels.hip; chemeleon.py:137-244)
+struct TrainArgs {
+  long N; int B, A, T;
+  const int64_t* t;        // [B] timestep per graph
+  const int64_t* a0; const float* x0; const float* l0;
+  const float* rand_a; const float* noise_l; const float* noise_x;  // [N,A], [B,3,3] (masked), [N,3]
+  const float* coef;       // [T+1][4]: sqrt(abar), sqrt(1 - abar), sigma_x, sigma_norm
+  const float* q_one_step; const float* q_mats;
+  const int* n2g;
+  int64_t* a_t; float* x_t; float* l_t; float* target_x;  // noised state, score target
+  const float* HO; const float* LAT;                  // decoder heads on the noised state
+  float* part;             // [N][2] per-node KL, CE
+  float hybrid, cost_a, cost_l, cost_x;
+  float* out;              // [6]: loss, vb, ce, loss_atom_types, loss_lattice, loss_coords
+};
+hipError_t train_noise(const TrainArgs& g, hipStream_t s);
+hipError_t train_loss(const TrainArgs& g, hipStream_t s);
 hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm_init();
 // the same kernels on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)

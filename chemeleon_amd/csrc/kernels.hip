@@ -691,4 +691,192 @@ hipError_t step_corrector(const StepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Training forward / validation loss (chemeleon.py:137-244): q_sample of the state at per-graph t,
+// then (after the decoder) the D3PM hybrid loss, the lattice and coordinate MSEs.
+// ---------------------------------------------------------------------------
+// d_log_p_wrapped_normal(x, sigma) (diff_utils.py:35-47): 21 wrapped terms, the reference's order
+__device__ __forceinline__ float dlogp_wrapped(float x, float s) {
+  const float s2 = __fmul_rn(s, s);
+  float num = 0.f, den = 0.f;
+  for (int i = -10; i <= 10; ++i) {
+    const float u = __fadd_rn(x, (float)i);
+    const float e = expf(__fdiv_rn(__fdiv_rn(-__fmul_rn(u, u), 2.0f), s2));
+    num = __fadd_rn(num, __fmul_rn(__fdiv_rn(u, s2), e));
+    den = __fadd_rn(den, e);
+  }
+  return __fdiv_rn(num, den);
+}
+
+// one wave per node: x_t atom type (q_sample: argmax of log(q_mats[t-1][a0] + eps) + Gumbel),
+// x_t coordinates ((x0 + sigma z) % 1) and the score target d_log_p(sigma z, sigma) / sqrt(sigma_norm)
+__global__ __launch_bounds__(256) void k_train_noise(TrainArgs g) {
+  const int lane = threadIdx.x & 63;
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= g.N) return;
+  const int A = g.A, gph = g.n2g[i];
+  const int t = (int)g.t[gph];
+  const float eps = 1.0e-6f;
+  const int x0 = (int)g.a0[i];
+  const float* Q = g.q_mats + ((long)(t - 1) * A + x0) * A;
+  float bv = -INFINITY;
+  int bi = 0;
+  for (int d = lane; d < A; d += 64) {
+    const float lg = logf(__fadd_rn(Q[d], eps));
+    const float u = fminf(fmaxf(g.rand_a[i * A + d], eps), 1.0f);
+    const float v = __fadd_rn(lg, -logf(-logf(u)));
+    if (better(v, d, bv, bi)) { bv = v; bi = d; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) g.a_t[i] = bi;
+  if (lane < 3) {
+    const float* cf = g.coef + (long)t * 4;  // {sqrt(abar), sqrt(1 - abar), sigma_x, sigma_norm}
+    const float sz = __fmul_rn(cf[2], g.noise_x[i * 3 + lane]);
+    g.x_t[i * 3 + lane] = rem1(__fadd_rn(g.x0[i * 3 + lane], sz));
+    g.target_x[i * 3 + lane] = __fdiv_rn(dlogp_wrapped(sz, cf[2]), sqrtf(cf[3]));
+  }
+}
+
+// l_t = sqrt(abar) l0 + sqrt(1 - abar) noise (noise already masked), one thread per entry
+__global__ void k_train_lattice(TrainArgs g) {
+  const long k = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (long)g.B * 9) return;
+  const float* cf = g.coef + g.t[k / 9] * 4;
+  g.l_t[k] = __fadd_rn(__fmul_rn(cf[0], g.l0[k]), __fmul_rn(cf[1], g.noise_l[k]));
+}
+
+// one wave per node: true and predicted posterior logits (q_posterior_logits, diff_utils.py:258-286),
+// KL(true || pred) (categorical_kl_logits, :288-305) and -log_softmax(pred)[a0] (cross entropy)
+__global__ __launch_bounds__(256) void k_train_node_loss(TrainArgs g) {
+  __shared__ float sm_all[4][128];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sm = sm_all[wv];
+  const long i = (long)blockIdx.x * 4 + wv;
+  if (i >= g.N) return;
+  const int A = g.A, T = g.T;
+  const int t = (int)g.t[g.n2g[i]];
+  const float eps = 1.0e-6f;
+  const int x0 = (int)g.a0[i], xt = (int)g.a_t[i];
+  const int d0 = lane, d1 = lane + 64;
+  const bool ok1 = d1 < A;
+  const float* P = g.HO + i * HEADS_N;  // predicted x_0 logits (types head)
+  const float lg0 = P[d0], lg1 = ok1 ? P[d1] : -INFINITY;
+  // softmax of the prediction
+  const float mx = wave_max(fmaxf(lg0, lg1));
+  const float e0 = expf(lg0 - mx), e1 = ok1 ? expf(lg1 - mx) : 0.f;
+  const float se = wave_sum(e0 + e1);
+  sm[d0] = e0 / se;
+  if (ok1) sm[d1] = e1 / se;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  // true x_0 logits: log(one_hot + eps); its softmax row is (1 + eps, eps, ...) normalised
+  const float tl0 = logf(__fadd_rn(d0 == x0 ? 1.0f : 0.0f, eps));
+  const float tl1 = ok1 ? logf(__fadd_rn(d1 == x0 ? 1.0f : 0.0f, eps)) : -INFINITY;
+  float q0 = lg0, q1 = lg1, p0 = tl0, p1 = tl1;  // (t == 1: the x_0 logits themselves)
+  if (t != 1) {
+    const long t2 = (t - 2 + (T + 1)) % (T + 1);
+    const float* Q2 = g.q_mats + t2 * A * A;
+    const float* Q1 = g.q_one_step + (long)(t - 1) * A * A;
+    // true: softmax(log(onehot + eps)) @ Q2; pred: softmax(pred) @ Q2
+    const float tmx = wave_max(fmaxf(tl0, tl1));
+    const float te0 = expf(tl0 - tmx), te1 = ok1 ? expf(tl1 - tmx) : 0.f;
+    const float tse = wave_sum(te0 + te1);
+    float fp0 = 0.f, fp1 = 0.f, ft0 = 0.f, ft1 = 0.f;
+    for (int cc = 0; cc < A; ++cc) {
+      const float p = sm[cc];
+      const float pt = __fdiv_rn(expf(logf(__fadd_rn(cc == x0 ? 1.0f : 0.0f, eps)) - tmx), tse);
+      fp0 = fmaf(p, Q2[cc * A + d0], fp0);
+      ft0 = fmaf(pt, Q2[cc * A + d0], ft0);
+      if (ok1) {
+        fp1 = fmaf(p, Q2[cc * A + d1], fp1);
+        ft1 = fmaf(pt, Q2[cc * A + d1], ft1);
+      }
+    }
+    const float f10 = logf(__fadd_rn(Q1[d0 * A + xt], eps));
+    q0 = __fadd_rn(f10, logf(__fadd_rn(fp0, eps)));
+    p0 = __fadd_rn(f10, logf(__fadd_rn(ft0, eps)));
+    if (ok1) {
+      const float f11 = logf(__fadd_rn(Q1[d1 * A + xt], eps));
+      q1 = __fadd_rn(f11, logf(__fadd_rn(fp1, eps)));
+      p1 = __fadd_rn(f11, logf(__fadd_rn(ft1, eps)));
+    }
+  }
+  // KL(C(p) || C(q)) with both logits shifted by eps (categorical_kl_logits)
+  const float a0 = p0 + eps, a1 = ok1 ? p1 + eps : -INFINITY;
+  const float b0 = q0 + eps, b1 = ok1 ? q1 + eps : -INFINITY;
+  const float am = wave_max(fmaxf(a0, a1)), bm = wave_max(fmaxf(b0, b1));
+  const float ea0 = expf(a0 - am), ea1 = ok1 ? expf(a1 - am) : 0.f;
+  const float eb0 = expf(b0 - bm), eb1 = ok1 ? expf(b1 - bm) : 0.f;
+  const float lsa = logf(wave_sum(ea0 + ea1)) + am, lsb = logf(wave_sum(eb0 + eb1)) + bm;
+  const float sa = wave_sum(ea0 + ea1);
+  float kl = (ea0 / sa) * ((a0 - lsa) - (b0 - lsb));
+  if (ok1) kl += (ea1 / sa) * ((a1 - lsa) - (b1 - lsb));
+  kl = wave_sum(kl);
+  // cross entropy of the predicted x_0 logits at a0
+  const float lse = logf(se) + mx;
+  const float mine = (d0 == x0 ? lg0 : 0.f) + (ok1 && d1 == x0 ? lg1 : 0.f);
+  const float ce = lse - wave_sum(mine);
+  if (lane == 0) {
+    g.part[i * 2 + 0] = kl;
+    g.part[i * 2 + 1] = ce;
+  }
+}
+
+// one block: the means (fixed summation order) and the weighted total
+__global__ __launch_bounds__(256) void k_train_reduce(TrainArgs g) {
+  __shared__ float red[4][256];
+  const int tid = threadIdx.x;
+  float kl = 0.f, ce = 0.f, ex = 0.f, el = 0.f;
+  for (long i = tid; i < g.N; i += 256) {
+    kl += g.part[i * 2];
+    ce += g.part[i * 2 + 1];
+    for (int k = 0; k < 3; ++k) {
+      const float d = g.HO[i * HEADS_N + g.A + k] - g.target_x[i * 3 + k];
+      ex += d * d;
+    }
+  }
+  for (long k = tid; k < (long)g.B * 9; k += 256) {
+    const int e = (int)(k % 9);
+    if (e == 1 || e == 6 || e == 7) continue;  // mask [[1,0,1],[1,1,1],[0,0,1]] (chemeleon.py:70-72)
+    const float d = g.LAT[k] - g.noise_l[k];
+    el += d * d;
+  }
+  red[0][tid] = kl; red[1][tid] = ce; red[2][tid] = ex; red[3][tid] = el;
+  __syncthreads();
+  if (tid < 4) {
+    float sacc = 0.f;
+    for (int k = 0; k < 256; ++k) sacc += red[tid][k];
+    red[tid][0] = sacc;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float vb = red[0][0] / (float)g.N, cel = red[1][0] / (float)g.N;
+    const float lx = red[2][0] / (float)(3 * g.N), ll = red[3][0] / (float)(6 * g.B);
+    const float la = vb + cel * g.hybrid;
+    g.out[0] = g.cost_a * la + g.cost_l * ll + g.cost_x * lx;
+    g.out[1] = vb;
+    g.out[2] = cel;
+    g.out[3] = la;
+    g.out[4] = ll;
+    g.out[5] = lx;
+  }
+}
+
+hipError_t train_noise(const TrainArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_train_noise, dim3((unsigned)((g.N + 3) / 4)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_train_lattice, dim3((unsigned)((g.B * 9 + 255) / 256)), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t train_loss(const TrainArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_train_node_loss, dim3((unsigned)((g.N + 3) / 4)), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_train_reduce, dim3(1), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
 }  // namespace chm

@@ -1120,6 +1120,41 @@ extern "C" int chm_edge_features(chm_batch* b, const float* x, float* feat, void
   return CHM_OK;
 }
 
+extern "C" int chm_training_loss(chm_batch* b, const chm_train_tables* tt, const int64_t* d_t, const int64_t* a0,
+                                 const float* x0, const float* l0, const float* temb, const float* text,
+                                 const float* rand_a, const float* noise_l, const float* noise_x, float* out,
+                                 int64_t* a_t, float* x_t, float* l_t, float* target_x, float* pred_lattice,
+                                 float* pred_coords, void* stream) {
+  if (!b || !tt || !d_t || !a0 || !x0 || !l0 || !rand_a || !noise_l || !noise_x || !out)
+    return fail(CHM_E_ARG, "NULL argument");
+  if (!a_t || !x_t || !l_t || !target_x) return fail(CHM_E_ARG, "the noised-state outputs are required");
+  if (!tt->d_coef4 || !tt->d_q_one_step || !tt->d_q_mats || tt->T < 1) return fail(CHM_E_ARG, "bad tables");
+  const chm_model* m = b->m;
+  if (!m->film || !temb) return fail(CHM_E_ARG, "the training forward needs a time-conditioned decoder");
+  if (m->d.text_dim > 0 && !text) return fail(CHM_E_ARG, "text embeddings required (text_dim > 0)");
+  hipStream_t s = (hipStream_t)stream;
+  const long N = b->N;
+  const int B = b->B;
+  TrainArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.N = N; g.B = B; g.A = m->d.max_atoms; g.T = tt->T; g.t = d_t; g.a0 = a0; g.x0 = x0; g.l0 = l0;
+  g.rand_a = rand_a; g.noise_l = noise_l; g.noise_x = noise_x; g.coef = tt->d_coef4;
+  g.q_one_step = tt->d_q_one_step; g.q_mats = tt->d_q_mats; g.n2g = b->n2g;
+  g.a_t = a_t; g.x_t = x_t; g.l_t = l_t; g.target_x = target_x;
+  g.hybrid = tt->hybrid_coeff; g.cost_a = tt->cost_atom_types; g.cost_l = tt->cost_lattice; g.cost_x = tt->cost_coords;
+  g.HO = b->HO; g.LAT = b->LAT; g.part = b->Y;  // (Y: decoder scratch, free after the call)
+  g.out = out;
+  HIPCHK(train_noise(g, s));
+  int rc = run_decoder(b, 1, a_t, x_t, l_t, temb, m->d.time_dim, nullptr, text, nullptr, 3, s);
+  if (rc) return rc;
+  HIPCHK(train_loss(g, s));
+  if (pred_lattice) HIPCHK(hipMemcpyAsync(pred_lattice, b->LAT, (size_t)B * 9 * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (pred_coords)
+    HIPCHK(hipMemcpy2DAsync(pred_coords, 3 * sizeof(float), b->HO + m->d.max_atoms, HEADS_N * sizeof(float),
+                            3 * sizeof(float), N, hipMemcpyDeviceToDevice, s));
+  return CHM_OK;
+}
+
 extern "C" int chm_knn_edges(chm_batch* b, const float* x, const float* lat, int32_t* src, int32_t* dst, float* fd,
                              int64_t capacity, int64_t* n_edges, void* stream) {
   if (!b || !x || !lat || !n_edges) return fail(CHM_E_ARG, "NULL argument");

@@ -30,6 +30,7 @@ downloaded). Alternatively pass any `text_encoder` object with the reference's
 `text_embeds=` / `null_text_embeds=` tensors directly.
 """
 
+import ctypes
 import os
 from typing import Any, Dict, Iterator, List, Optional, Tuple, Union
 
@@ -75,6 +76,88 @@ class Chemeleon(nn.Module):
                               max_neighbors=cfg["max_neighbors"], ln=cfg["ln"], ip=cfg["ip"], smooth=cfg["smooth"],
                               pred_atom_types=cfg["pred_atom_types"])
         self._tables: Dict[Tuple, Tuple] = {}
+
+    # ------------------------------------------------------------------ training forward
+    def forward(self, batch, noise=None) -> Dict[str, Any]:
+        """Training forward / validation loss (chemeleon.py:137-244) on the HIP path: per-graph t from
+        `beta_scheduler.uniform_sample_t` (numpy's global generator, as the reference), q_sample of
+        atom types (D3PM), lattices (variance preserving) and fractional coordinates (variance
+        exploding, score target d_log_p_wrapped_normal / sqrt(sigma_norm)), one decoder call, the D3PM
+        hybrid loss (KL of the posteriors + hybrid_coeff * cross entropy), lattice and coordinate MSEs.
+
+        `batch` has atom_types [N], frac_coords [N,3], lattices [B,3,3], natoms [B], batch [N] and,
+        for text-guided models, text (List[str]) (what Batch.from_data_list builds); `noise` =
+        (t [B], rand_a [N,A], noise_lattice [B,3,3] (unmasked), noise_coords [N,3]) or None to draw
+        them in the reference's order (t from numpy, the rest from the CPU torch generator).
+        Returns the reference's dict (loss, vb_loss_atom_types, ce_loss_atom_types, true / pred noise
+        lattice (masked entries), true / pred noise coords). No autograd: the HIP decoder has no
+        backward pass."""
+        dev = self.device
+        if dev.type != "cuda":
+            raise RuntimeError("Chemeleon (chemeleon_amd) runs on a HIP device only; call .to('cuda') first")
+        natoms = [int(n) for n in (batch.natoms.tolist() if torch.is_tensor(batch.natoms) else batch.natoms)]
+        B, N, A, T = len(natoms), sum(natoms), self.max_atoms, self.num_timesteps
+        mask = self.mask_lattice_matrix
+        if noise is None:
+            t = self.beta_scheduler.uniform_sample_t(B, "cpu")  # chemeleon.py:147
+            rand_a = torch.rand(N, A)  # :162-164
+            nl = torch.randn(B, 3, 3)  # :170 (randn_like(l_0))
+            nx = torch.randn(N, 3)  # :175 (randn_like(frac_coords))
+        else:
+            t, rand_a, nl, nx = noise
+        nl = (nl.float().cpu() * mask).to(dev).contiguous()
+        t = torch.as_tensor(t).long().to(dev).contiguous()
+        rand_a = rand_a.float().to(dev).contiguous()
+        nx = nx.float().to(dev).contiguous()
+        a0 = batch.atom_types.long().to(dev).contiguous()
+        x0 = batch.frac_coords.float().to(dev).contiguous()
+        l0 = batch.lattices.float().to(dev).contiguous()
+        te = self.time_embed(t).float().contiguous()  # :149
+        text = None
+        if self.text_guide:  # :186-191 (cond_drop_prob applies, as in training)
+            if self.text_encoder is None:
+                raise RuntimeError("text_guide model: pass text_encoder=... to compute the training loss")
+            text = self.text_encoder.get_text_embeds(list(batch.text), self.cond_drop_prob, device=dev)
+            text = text.float().to(dev).contiguous()
+        tt, _keep = self._train_tables()
+        out = torch.empty(6, device=dev)
+        a_t = torch.empty(N, dtype=torch.long, device=dev)
+        x_t = torch.empty(N, 3, device=dev)
+        l_t = torch.empty(B, 3, 3, device=dev)
+        target = torch.empty(N, 3, device=dev)
+        pl = torch.empty(B, 3, 3, device=dev)
+        pc = torch.empty(N, 3, device=dev)
+        b = self.decoder.hip_batch(natoms, max_pairs=1)
+        P = _lib.ptr
+        _lib.require_device(t, a0, x0, l0, te, text, rand_a, nl, nx)
+        _lib.check(_lib.load().chm_training_loss(b.handle, ctypes.byref(tt), P(t), P(a0), P(x0), P(l0), P(te), P(text),
+                                                 P(rand_a), P(nl), P(nx), P(out), P(a_t), P(x_t), P(l_t), P(target),
+                                                 P(pl), P(pc), _lib.stream_handle(dev)), "chm_training_loss")
+        m = mask.to(dev)
+        return {"loss": out[0], "vb_loss_atom_types": out[1], "ce_loss_atom_types": out[2],
+                "true_noise_lattice": nl.masked_select(m), "pred_noise_lattice": pl.masked_select(m),
+                "true_noise_coords": target, "pred_noise_coords": pc,
+                "loss_atom_types": out[3], "loss_lattice": out[4], "loss_coords": out[5],
+                "x_t_atom_types": a_t, "x_t_coords": x_t, "x_t_lattice": l_t}
+
+    def _train_tables(self):
+        """Device tables of the training forward: {sqrt(abar_t), sqrt(1 - abar_t), sigma_t,
+        sigmas_norm_t} per t (the reference's fp32 expressions, chemeleon.py:151-157) and the D3PM
+        matrices; cached per device."""
+        dev = self.device
+        key = ("train", str(dev))
+        if key not in self._tables:
+            ac = self.beta_scheduler.alphas_cumprod.float().cpu()
+            coef = torch.stack([torch.sqrt(ac), torch.sqrt(1.0 - ac), self.sigma_scheduler.sigmas.float().cpu(),
+                                self.sigma_scheduler.sigmas_norm.float().cpu()], dim=1).contiguous().to(dev)
+            q1 = self.d3pm.q_one_step_mats.float().contiguous().to(dev)
+            qm = self.d3pm.q_mats.float().contiguous().to(dev)
+            h = self.hparams
+            tt = _lib.chm_train_tables(self.num_timesteps, _lib.ptr(coef), _lib.ptr(q1), _lib.ptr(qm),
+                                       float(self.d3pm.hybrid_coeff), float(h["cost_atom_types"]),
+                                       float(h["cost_lattice"]), float(h["cost_coords"]))
+            self._tables[key] = (tt, (coef, q1, qm))
+        return self._tables[key]
 
     @staticmethod
     def _build_text_encoder(cfg, kwargs):

@@ -176,6 +176,29 @@ int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* d_atom_types, co
                         float* d_types_out, float* d_lattice_out, float* d_coords_out, float* d_node_out,
                         void* stream);
 
+/* Training forward / validation loss (Chemeleon.forward, chemeleon.py:137-244) for a batch created
+ * with max_pairs >= 1: q_sample of (d_a0, d_x0, d_l0) at the per-graph timesteps d_t [B] (int64,
+ * 1..T) with the caller's noise (d_rand_a [N,A] uniforms, d_noise_l [B,3,3] normals already masked by
+ * [[1,0,1],[1,1,1],[0,0,1]], d_noise_x [N,3] normals), one decoder call on the noised state with
+ * d_time_emb [B,time_dim] and d_text [B,text_dim] (or NULL), then the D3PM hybrid loss, lattice and
+ * coordinate MSEs. Tables (device fp32): d_coef4 [T+1][4] = {sqrt(abar_t), sqrt(1 - abar_t),
+ * sigma_t, sigmas_norm_t}, d_q_one_step / d_q_mats [T+1][A][A] as in chm_schedule.
+ * Outputs: d_out[6] = {loss, vb_loss, ce_loss, loss_atom_types, loss_lattice, loss_coords};
+ * optional (NULL to skip) d_a_t [N] int64, d_x_t [N,3], d_l_t [B,3,3], d_target_x [N,3] (the score
+ * target), d_pred_lattice [B,3,3], d_pred_coords [N,3]. */
+typedef struct chm_train_tables {
+  int T;
+  const float* d_coef4;
+  const float* d_q_one_step;
+  const float* d_q_mats;
+  float hybrid_coeff, cost_atom_types, cost_lattice, cost_coords;
+} chm_train_tables;
+int chm_training_loss(chm_batch* b, const chm_train_tables* tt, const int64_t* d_t, const int64_t* d_a0,
+                      const float* d_x0, const float* d_l0, const float* d_time_emb, const float* d_text,
+                      const float* d_rand_a, const float* d_noise_l, const float* d_noise_x, float* d_out,
+                      int64_t* d_a_t, float* d_x_t, float* d_l_t, float* d_target_x, float* d_pred_lattice,
+                      float* d_pred_coords, void* stream);
+
 /* Per-timestep schedule tables (device, fp32), computed once by the host from
  * the reference schedules (diff_utils.py:57-131, chemeleon.py:413-457):
  *   d_coef [T+1][8]: {c0, c1, sigma_l, step_x, std_x, sqrt(sigma_norm),

@@ -121,6 +121,30 @@ def d3pm_p_sample(pred_logits, x_t, t_per_node, noise, q_one_step, q_mats):
     return torch.argmax(post + g * nz, dim=-1)
 
 
+def d3pm_q_sample(x0, t_per_node, noise, q_mats):
+    """diff_utils.py:236-256 — Categorical(x_0 Q_{1..t}) through the Gumbel argmax."""
+    logits = torch.log(q_mats[t_per_node - 1, x0, :] + EPS)
+    noise = torch.clip(noise, EPS, 1.0)
+    return torch.argmax(logits + -torch.log(-torch.log(noise)), dim=-1)
+
+
+def d3pm_q_posterior_logits(x0, x_t, t_per_node, q_one_step, q_mats, x0_is_logits: bool):
+    """diff_utils.py:258-286 — logits of q(x_{t-1} | x_t, x_0); x_0 as indices (one-hot, + eps, log)
+    or as logits (`is_x_0_one_hot=True` in the reference's naming)."""
+    A = q_mats.shape[-1]
+    x0_logits = x0.clone() if x0_is_logits else torch.log(F.one_hot(x0, A) + EPS)
+    fact1 = q_one_step.transpose(1, 2)[t_per_node - 1, x_t, :]
+    fact2 = torch.einsum("bc,bcd->bd", torch.softmax(x0_logits, dim=-1), q_mats[t_per_node - 2])
+    out = torch.log(fact1 + EPS) + torch.log(fact2 + EPS)
+    return torch.where((t_per_node == 1)[:, None], x0_logits, out)
+
+
+def categorical_kl_logits(l1, l2, eps=1.0e-6):
+    """diff_utils.py:288-305 — mean over rows of KL(C(l1) || C(l2)), logits shifted by eps."""
+    out = torch.softmax(l1 + eps, dim=-1) * (torch.log_softmax(l1 + eps, dim=-1) - torch.log_softmax(l2 + eps, dim=-1))
+    return out.sum(dim=-1).mean()
+
+
 # ----------------------------------------------------------------------------
 # score network  (chemeleon/modules/cspnet.py)
 # ----------------------------------------------------------------------------
@@ -291,6 +315,37 @@ class OracleModel:
         std2 = torch.sqrt(2 * step2)
         x_prev = x_half - step2 * (px2 * torch.sqrt(sn)) + std2 * rx2
         return a_prev, x_prev % 1.0, l_prev, x_half
+
+    def training_forward(self, a0, x0, l0, natoms, t, rand_a, noise_l, noise_x, text):
+        """chemeleon.py:137-244 with the draws given: t [B], rand_a [N,A], noise_l [B,3,3] (unmasked),
+        noise_x [N,3]; `text` [B, text_dim] as get_text_embeds returned it. Returns the loss dict."""
+        nat = torch.as_tensor([int(n) for n in natoms])
+        B = len(nat)
+        n2g = torch.arange(B).repeat_interleave(nat)
+        te = time_embedding(t, self.cfg["time_dim"])
+        ac = self.beta["alphas_cumprod"][t]
+        c0, c1 = torch.sqrt(ac), torch.sqrt(1.0 - ac)
+        sig, sn = self.sigmas[t], self.sigmas_norm[t]
+        tn = t[n2g]
+        a_t = d3pm_q_sample(a0, tn, rand_a, self.q_mats)
+        nl = noise_l * LATTICE_MASK
+        l_t = c0[:, None, None] * l0 + c1[:, None, None] * nl
+        s_a, sn_a = sig[n2g][:, None], sn[n2g][:, None]
+        target = d_log_p_wrapped_normal(s_a * noise_x, s_a) / torch.sqrt(sn_a)
+        x_t = (x0 + s_a * noise_x) % 1.0
+        types, lat, coords, _ = self.decoder(te, a_t, x_t, l_t, nat, n2g, text)
+        true_post = d3pm_q_posterior_logits(a0, a_t, tn, self.q_one_step, self.q_mats, False)
+        pred_post = d3pm_q_posterior_logits(types, a_t, tn, self.q_one_step, self.q_mats, True)
+        vb = categorical_kl_logits(true_post, pred_post)
+        ce = F.cross_entropy(types, a0)
+        la = vb + ce * self.cfg.get("d3pm_hybrid_coeff", 1.0)
+        ll = F.mse_loss(lat.masked_select(LATTICE_MASK), nl.masked_select(LATTICE_MASK))
+        lx = F.mse_loss(coords, target)
+        loss = (self.cfg.get("cost_atom_types", 1.0) * la + self.cfg.get("cost_lattice", 1.0) * ll
+                + self.cfg.get("cost_coords", 1.0) * lx)
+        return {"loss": loss, "vb_loss_atom_types": vb, "ce_loss_atom_types": ce,
+                "true_noise_lattice": nl.masked_select(LATTICE_MASK), "pred_noise_lattice": lat.masked_select(LATTICE_MASK),
+                "true_noise_coords": target, "pred_noise_coords": coords, "x_t_atom_types": a_t}
 
     def draw_noise(self, t: int, N: int, B: int):
         """RNG order of chemeleon.py:400-404,418,435,455 on the global CPU

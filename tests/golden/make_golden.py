@@ -448,6 +448,35 @@ def gen_knn(chm, csp):
     save("knn.npz", **rec)
 
 
+TRAIN_T = [1, 2, 500, 1000, 37, 999, 250, 3]
+
+
+def gen_train(chm, csp):
+    """Chemeleon.forward (chemeleon.py:137-244), the training forward / validation loss, run by the
+    reference itself: t per graph fixed through its uniform_sample_t (which draws from numpy), the
+    q_sample / noise draws from the CPU torch generator seeded right before the call (the test redraws
+    them from the seed in the reference's order), cond_drop_prob = 0 (the stub encoder's cond)."""
+    m, sd = build_reference_model(chm, csp, 1000)
+    m.cond_drop_prob = 0.0
+    natoms = [6, 9, 4, 12, 1, 7, 5, 8]
+    B, N = len(natoms), sum(natoms)
+    a, x, lat = knn_crystals(natoms, 51, 4.0, 7.0)
+    nat = torch.tensor(natoms)
+    batch = types.SimpleNamespace(num_graphs=B, num_nodes=N, batch=torch.arange(B).repeat_interleave(nat),
+                                  atom_types=a, frac_coords=x, lattices=lat * torch.tensor([[1, 0, 1], [1, 1, 1], [0, 0, 1]]),
+                                  natoms=nat, text=["x"] * B)
+    m.beta_scheduler.uniform_sample_t = lambda bs, device: torch.tensor(TRAIN_T[:bs])
+    torch.manual_seed(77)
+    with torch.no_grad():
+        out = m(batch)
+    rec = {"natoms": nat, "atom_types": a, "frac": x, "lattices": batch.lattices, "t": torch.tensor(TRAIN_T),
+           "noise_seed": np.int64(77), "weights_crc": weights_crc(sd)}
+    for k, v in out.items():
+        rec["out_" + k] = v
+    save("train_forward.npz", **rec)
+    print({k: float(v) for k, v in out.items() if v.dim() == 0})
+
+
 CLIP_DIM = 256
 
 
@@ -644,6 +673,8 @@ if __name__ == "__main__":
         gen_text(chm, csp)
     if "knn" in which:
         gen_knn(chm, csp)
+    if "train" in which:
+        gen_train(chm, csp)
     if "clip_graph" in which:
         gen_clip_graph(chm, csp)
     if "trajectory1000" in which:
