@@ -370,6 +370,10 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_split = value != 0;
     return CHM_OK;
   }
+  if (k == "edge16") {  // (batches created afterwards; knn batches need the k_edge16 kernels)
+    m->edge16 = value != 0;
+    return CHM_OK;
+  }
   return fail(CHM_E_ARG, "unknown option: " + k);
 }
 

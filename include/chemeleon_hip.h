@@ -80,10 +80,11 @@ int chm_model_create(const chm_dims* dims, const float* const* d_params, int n_p
                      chm_model** out);
 void chm_model_destroy(chm_model* m);
 
-/* Launch-schedule options (results are bit-identical either way; not thread-safe against
- * concurrent steps of the same model):
+/* Launch-schedule options (not thread-safe against concurrent steps of the same model):
  *   "edge_split" (0 / 1): when edge layer 1's 256x256 tiles leave a partial last round of the
  *     grid, run that round in one grid with the edge-layer-2 tiles that do not read its rows.
+ *   "edge16" (1 / 0): split16 edge GEMMs on v_mfma_f32_16x16x32_f16 (k_edge16, default) or on the
+ *     round-1 32x32x16 kernels (k_edge_gemm); same arithmetic up to the MFMA's summation order.
  * Returns CHM_E_ARG for an unknown key. */
 int chm_model_set_option(chm_model* m, const char* key, int64_t value);
 

@@ -262,6 +262,30 @@ def test_edge_tail_split_is_bit_identical(cn, nat):
         assert torch.equal(u, v), f"{what}: split and one-launch-per-layer edge schedules differ"
 
 
+@pytest.mark.parametrize("tag", ["64x20", "16x40"])
+def test_teacher_forced_steps_edge32_kernels(golden, cn, tag):
+    """The round-1 split16 edge kernels (v_mfma_f32_32x32x16_f16, k_edge_gemm; option edge16 = 0)
+    stay a tested arm: one step against the reference fixtures, same gates."""
+    model = _model(1000)
+    model.decoder.set_option("edge16", 0)
+    g = golden(f"step_{tag}.npz")
+    nat = g["natoms"].tolist()
+    B, N = len(nat), sum(nat)
+    for t in g["ts"][:2]:
+        t = int(t)
+        torch.manual_seed(5000 + t)
+        nz = None
+        if t > 1:
+            nz = (torch.rand((N, 104)), torch.randn(B, 3, 3), torch.randn(N, 3), torch.randn(N, 3))
+        a, x, lat = model.reverse_step(t, torch.from_numpy(g[f"t{t}_a"]), torch.from_numpy(g[f"t{t}_x"]),
+                                       torch.from_numpy(g[f"t{t}_l"]), nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)
+        np.testing.assert_array_equal(a.cpu().numpy(), g[f"t{t}_a_out"], err_msg=f"atom types t={t}")
+        periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"frac t={t}")
+        close(lat.cpu(), g[f"t{t}_l_out"], what=f"lattice t={t}")
+    del model
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.timeout(300)
 def test_ragged_2048_full_size_step(model1000, cn):
     """configs[4] at full size on one GPU (2048 crystals, natoms = randint(1, 81, seed 7),
