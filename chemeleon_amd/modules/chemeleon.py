@@ -145,8 +145,13 @@ class Chemeleon(nn.Module):
         sigmas_norm_t} per t (the reference's fp32 expressions, chemeleon.py:151-157) and the D3PM
         matrices; cached per device."""
         dev = self.device
-        key = ("train", str(dev))
+        bufs = (self.beta_scheduler.alphas_cumprod, self.sigma_scheduler.sigmas, self.sigma_scheduler.sigmas_norm,
+                self.d3pm.q_one_step_mats, self.d3pm.q_mats)
+        key = ("train", str(dev), tuple((b.data_ptr(), b._version) for b in bufs),
+               tuple(float(self.hparams[k]) for k in ("cost_atom_types", "cost_lattice", "cost_coords")))
         if key not in self._tables:
+            for k in [k for k in self._tables if k[0] == "train"]:  # (one training entry at a time)
+                del self._tables[k]
             ac = self.beta_scheduler.alphas_cumprod.float().cpu()
             coef = torch.stack([torch.sqrt(ac), torch.sqrt(1.0 - ac), self.sigma_scheduler.sigmas.float().cpu(),
                                 self.sigma_scheduler.sigmas_norm.float().cpu()], dim=1).contiguous().to(dev)
