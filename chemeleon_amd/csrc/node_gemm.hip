@@ -19,7 +19,7 @@
 // grow ~10^4x over a 1000-step trajectory); 2^e_r is applied again in the epilogue.
 //
 // 128x128 tiles, 256 threads (4 waves of 64x64, C^T accumulators as in gemm_bf16x3.hip),
-// K-tiles of 16, a 4-deep ring of 20 KB stages (3 K-tiles in flight), two blocks per CU; S16 uses
+// K-tiles of 16, a 4-deep ring of 20 KB stages (4 K-tiles in flight), two blocks per CU; S16 uses
 // 16 KB stages, 5 deep with two blocks per CU or 3 deep with three (large grids).
 // LDS image per stage: A [128 rows][4 pieces of 4 fp32], piece p of row r at p ^ ((r >> 2) & 3);
 // W plane q [128 rows][2 pieces of 8 bf16], piece p of row r at p ^ ((r >> 3) & 1): the
@@ -71,7 +71,9 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 template <int VAR, bool S16, int NB>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   static_assert(NB == 2 || (S16 && NB == 3), "blocks per CU");
-  constexpr int STB_ = STB<S16>, NST_ = NST<S16, NB>, AHEAD = NST_ - 1;  // K-tiles in flight
+  // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
+  // step t's barrier it takes tile t + NST while tiles t+1 .. t+NST-1 are in flight or landed.
+  constexpr int STB_ = STB<S16>, NST_ = NST<S16, NB>, AHEAD = NST_;
   constexpr int GL = S16 ? 4 : 5;                                        // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage has been read
     asm volatile("" ::: "memory");
-    issue(t + AHEAD);                                 // past the end: re-reads into the free stage
+    issue(t + AHEAD);                                 // into tile t's stage; past the end: re-reads
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
     if constexpr (S16) {
