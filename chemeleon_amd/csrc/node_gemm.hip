@@ -20,7 +20,10 @@
 //
 // 128x128 tiles, 256 threads (4 waves of 64x64, C^T accumulators as in gemm_bf16x3.hip),
 // K-tiles of 16, a 4-deep ring of 20 KB stages (4 K-tiles in flight), two blocks per CU; S16 uses
-// 16 KB stages, 5 deep with two blocks per CU or 3 deep with three (large grids).
+// 16 KB stages, 5 deep with two blocks per CU or 3 deep with three (large grids). Small grids
+// (S16, NMT = 64): 64x128 tiles (4 waves of 32x64), 12 KB stages, 4 deep with three blocks per CU
+// or 3 deep with four: twice the blocks of the 128-row tiling, so the per-GPU shard's node GEMMs
+// (M = 5120: 160 blocks of 128 rows on 256 CUs, one wave per SIMD) fill the chip.
 // LDS image per stage: A [128 rows][4 pieces of 4 fp32], piece p of row r at p ^ ((r >> 2) & 3);
 // W plane q [128 rows][2 pieces of 8 bf16], piece p of row r at p ^ ((r >> 3) & 1): the
 // fragment reads of every 16-lane group then cover all 64 banks.
@@ -38,17 +41,20 @@ typedef const __attribute__((address_space(1))) void gbl_void;
 
 namespace {
 
-constexpr int NM = 128, NN = 128, NK = 16;
+constexpr int NN = 128, NK = 16;
 constexpr int A_ROWB = NK * 4, W_ROWB = NK * 2;  // 64 B, 32 B
-constexpr int A_STB = NM * A_ROWB;               // 8 KB
 constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
+template <int NMT> constexpr int A_STB = NMT * A_ROWB;  // 8 KB (128 rows), 4 KB (64 rows)
 // bf16x3: A + three W planes (20 KB) x 4 stages; S16: A + W hi/lo rows (8 + 8 KB) x 5 stages
-template <bool S16> constexpr int STB = S16 ? A_STB + 2 * W_PLB : A_STB + 3 * W_PLB;
-// NB = blocks per CU: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of 16 KB)
-template <bool S16, int NB> constexpr int NST = NB == 3 ? 3 : (S16 ? 5 : 4);
+template <bool S16, int NMT = 128> constexpr int STB = S16 ? A_STB<NMT> + 2 * W_PLB : A_STB<NMT> + 3 * W_PLB;
+// NB = blocks per CU. 128-row tiles: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of
+// 16 KB); 64-row tiles (S16): 3 (4 stages of 12 KB) or 4 (3 stages)
+template <bool S16, int NB, int NMT = 128>
+constexpr int NST = NMT == 64 ? (NB == 3 ? 4 : 3) : NB == 3 ? 3 : (S16 ? 5 : 4);
 constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
 static_assert(STB<true> * NST<true, 2> <= NODE_LDS && STB<false> * NST<false, 2> <= NODE_LDS, "LDS");
 static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
+static_assert(3 * STB<true, 64> * NST<true, 3, 64> <= 160 * 1024 && 4 * STB<true, 64> * NST<true, 4, 64> <= 160 * 1024, "LDS");
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -68,13 +74,15 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 }  // namespace
 
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR, bool S16, int NB>
+template <int VAR, bool S16, int NB, int NMT = 128>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
-  static_assert(NB == 2 || (S16 && NB == 3), "blocks per CU");
+  static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4), "tiling");
+  constexpr int NM = NMT, NI = NMT / 64;  // tile rows; 32-row fragment groups per wave
+  constexpr int A_STB_ = A_STB<NMT>;
   // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
   // step t's barrier it takes tile t + NST while tiles t+1 .. t+NST-1 are in flight or landed.
-  constexpr int STB_ = STB<S16>, NST_ = NST<S16, NB>, AHEAD = NST_;
-  constexpr int GL = S16 ? 4 : 5;                                        // glds per thread and K-tile
+  constexpr int STB_ = STB<S16, NMT>, NST_ = NST<S16, NB, NMT>, AHEAD = NST_;
+  constexpr int GL = S16 ? 2 + NI : 5;                                   // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -86,16 +94,16 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
   const int nk = g.K / NK;
 
-  // ---- glds sources. A: instruction q (of 8) covers rows 16q + (L >> 2), LDS piece L & 3 holding
-  // logical piece (L & 3) ^ ((L >> 4) & 3); wave w issues q = 2w, 2w + 1.
+  // ---- glds sources. A: instruction q (of 8, or 4 for 64 rows) covers rows 16q + (L >> 2), LDS
+  // piece L & 3 holding logical piece (L & 3) ^ ((L >> 4) & 3); wave w issues q = NI w .. NI w + NI-1.
   // W: instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1 holding
   // logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
   const int alp = (lane & 3) ^ ((lane >> 4) & 3);
-  const float* asrc[2];
-  const float* asrc2[2];
+  const float* asrc[NI];
+  const float* asrc2[NI];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = 16 * (2 * wave + u) + (lane >> 2);
+  for (int u = 0; u < NI; ++u) {
+    const int r = 16 * (NI * wave + u) + (lane >> 2);
     const long ar = row0 + (r < nrows ? r : nrows - 1);
     asrc[u] = g.A + ar * g.lda + 4 * alp;
     asrc2[u] = g.A2 + ar * g.lda2 + 4 * alp - g.ksplit;
@@ -115,43 +123,45 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     if constexpr (S16) {
       const int q = 2 * wave + u;
       wsrc[u] = Wpl + (long)(n0 + 16 * q + (lane >> 2)) * 2 * g.K + 8 * alp;
-      wdst[u] = A_STB + q * 1024;
+      wdst[u] = A_STB_ + q * 1024;
     } else {
       const int q = 3 * wave + u, p = q >> 2, rq = q & 3;
       wsrc[u] = Wpl + p * wplane + (long)(n0 + 32 * rq + (lane >> 1)) * g.K + 8 * wlp;
-      wdst[u] = A_STB + p * W_PLB + 32 * rq * W_ROWB;
+      wdst[u] = A_STB_ + p * W_PLB + 32 * rq * W_ROWB;
     }
   }
   auto issue = [&](int t) {
     const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
     char* st = lds + (t % NST_) * STB_;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NI; ++u) {
       const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (2 * wave + u) * A_ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (NI * wave + u) * A_ROWB), 16, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < NWI; ++u)
       __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + (S16 ? 2 * k0 : k0)), (lds_void*)(st + wdst[u]), 16, 0, 0);
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[NI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  // fragment offsets: A row wm*64 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
+  // fragment offsets: A row wm*NM/2 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
   const int asw = (r32 >> 2) & 3, wsw = (r32 >> 3) & 1;
-  // S16: this lane's two A rows (wm*64 + 32i + r32) and their power-of-two scales
-  float asc[2] = {1.0f, 1.0f}, aun[2] = {1.0f, 1.0f};
+  // S16: this lane's A rows (wm*NM/2 + 32i + r32) and their power-of-two scales
+  float asc[NI], aun[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) asc[i] = aun[i] = 1.0f;
   if constexpr (S16) {
     if (g.amax) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int lr = wm * 64 + 32 * i + r32;
+      for (int i = 0; i < NI; ++i) {
+        const int lr = wm * (NM / 2) + 32 * i + r32;
         const long ar = row0 + (lr < nrows ? lr : nrows - 1);
         float m = g.amax[ar];
         if (g.amax2) m = fmaxf(m, g.amax2[ar]);
@@ -162,23 +172,23 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
       }
     }
   }
-  const int fa0 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
-  const int fa1 = (wm * 64 + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
-  const int fw = A_STB + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
-  const int fw16[2] = {A_STB + (wn * 64 + r32) * 64 + 16 * (h ^ asw),         // hi piece h
-                       A_STB + (wn * 64 + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
+  const int fa0 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
+  const int fa1 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
+  const int fw = A_STB_ + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
+  const int fw16[2] = {A_STB_ + (wn * 64 + r32) * 64 + 16 * (h ^ asw),         // hi piece h
+                       A_STB_ + (wn * 64 + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
 
   // Software pipeline (VAR 0): while the 24 MFMAs of K-tile t run, the fragments of tile t+1 are
   // read from LDS and its A part is split, both interleaved between the MFMAs (the split's VALU
   // issues in the MFMAs' shadow). Fragment sets alternate, so the loop is unrolled by two.
   constexpr int NP = S16 ? 2 : 3;  // operand parts
   typedef std::conditional_t<S16, f16x8, bf16x8> frag;
-  f32x4 ra0[2], ra1[2];
-  frag fa[2][NP][2], fwt[2][NP][2];  // [set][part][i / j]
+  f32x4 ra0[NI], ra1[NI];
+  frag fa[2][NP][NI], fwt[2][NP][2];  // [set][part][i / j]
   auto read_raw = [&](int t, int set) {
     const char* st = lds + (t % NST_) * STB_;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       ra0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
       ra1[i] = *reinterpret_cast<const f32x4*>(st + fa1 + i * 32 * A_ROWB);
     }
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   };
   auto split = [&](int set) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
       if constexpr (S16) {
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
@@ -224,7 +234,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 #pragma unroll
     for (int k = k0; k < k1; ++k)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if constexpr (S16)
@@ -253,17 +263,17 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
     if constexpr (S16) {
-      mfmas(cur, 0, 1);                               // 4 MFMAs beside the 8 fragment reads
+      mfmas(cur, 0, 1);                               // 2 NI MFMAs beside the 4 + 2 NI fragment reads
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < 2 * NI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NI == 2 ? 2 : 3, 0);
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       split(cur ^ 1);
-      mfmas(cur, 1, 3);                               // 8 MFMAs, the split's VALU between them
+      mfmas(cur, 1, 3);                               // 4 NI MFMAs, the split's VALU between them
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < 4 * NI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
         __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
       }
@@ -292,11 +302,11 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the block exits
 
-  // lane l owns output row wm*64 + 32i + (l & 31) and, per 4-register group q, the four
+  // lane l owns output row wm*NM/2 + 32i + (l & 31) and, per 4-register group q, the four
   // consecutive columns wn*64 + 32j + 8q + 4h .. +3
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long lr = wm * 64 + i * 32 + r32;
+  for (int i = 0; i < NI; ++i) {
+    const long lr = wm * (NM / 2) + i * 32 + r32;
     float cm = 0.f;  // max |C| over this lane's columns of the row
     if (lr < nrows) {
       const long row = row0 + lr;
@@ -331,19 +341,23 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 
 int g_node_variant = 0;
 
+constexpr int LDS3 = STB<true> * NST<true, 3>;
+constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
+
 hipError_t node_gemm_init() {
-  const void* ks[6] = {(const void*)k_node_gemm<0, false, 2>, (const void*)k_node_gemm<1, false, 2>,
-                       (const void*)k_node_gemm<0, true, 2>,  (const void*)k_node_gemm<1, true, 2>,
-                       (const void*)k_node_gemm<0, true, 3>,  (const void*)k_node_gemm<1, true, 3>};
-  constexpr int L3 = STB<true> * NST<true, 3>;
-  const int bytes[6] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, L3, L3};
+  const void* ks[10] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
+                        (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
+                        (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
+                        (const void*)k_node_gemm<0, true, 3, 64>, (const void*)k_node_gemm<1, true, 3, 64>,
+                        (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>};
+  const int bytes[10] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  for (int i = 0; i < 10 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
-constexpr int LDS3 = STB<true> * NST<true, 3>;
+int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
@@ -356,12 +370,24 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const long blocks = ((g.M + NM - 1) / NM) * (g.N / NN);
+  const long blocks = ((g.M + 127) / 128) * (g.N / NN);
   const dim3 grid((unsigned)blocks), block(256);
   const bool v1 = g_node_variant == 1;
-  // S16: three blocks per CU (3 stages each) once the grid fills a round of them: more waves to hide
-  // the K-loop latency (-7% at M = 40960); small grids keep two blocks and 5 stages
-  const int nb = g_node_blocks ? g_node_blocks : (blocks >= 3 * 256 ? 3 : 2);
+  // S16, grids short of one 128-row block per CU: 64-row tiles (twice the blocks; M = 5120: 23 vs
+  // 26 us at K = 512); above that 128-row tiles at three blocks per CU (M = 20480: 54 vs 65 us with
+  // two), profiles/r2/node/node64_micro.log
+  const int rows = g_node_rows ? g_node_rows : (blocks < 256 ? 64 : 128);
+  if (g.wscale && rows == 64) {
+    const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
+    if (g_node_blocks == 4)
+      hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 4, 64> : k_node_gemm<0, true, 4, 64>), grid64, block, LDS64_4, s, g);
+    else
+      hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3, 64> : k_node_gemm<0, true, 3, 64>), grid64, block, LDS64_3, s, g);
+    return hipGetLastError();
+  }
+  // S16: three blocks per CU (3 stages each): more waves to hide the K-loop latency (-7% at
+  // M = 40960, -17% at M = 20480 against two blocks with 5 stages)
+  const int nb = g_node_blocks ? g_node_blocks : 3;
   if (g.wscale && nb == 3)
     hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3> : k_node_gemm<0, true, 3>), grid, block, LDS3, s, g);
   else if (g.wscale)

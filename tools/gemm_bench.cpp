@@ -183,13 +183,28 @@ int main(int argc, char** argv) {
         float t = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
         GemmArgs g0 = g16; g0.bias = nullptr; g0.act = 0;
         float t0 = time_it(50, s, [&] { CK(node_gemm(g0, s)); });
-        g_node_blocks = 2;
-        float t2 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
-        g_node_blocks = 3;
-        float t3 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
-        g_node_blocks = 0;
-        printf("M=%ld N=%d K=%d: default %.2f us (no bias/act %.2f us) | 2 blocks/CU %.2f us | 3 blocks/CU %.2f us\n", M,
-               N, k, t * 1e3, t0 * 1e3, t2 * 1e3, t3 * 1e3);
+        float tr[2][3];  // [64 / 128 rows][2, 3, 4 blocks per CU]
+        for (int r = 0; r < 2; ++r)
+          for (int nb = 2; nb <= 4; ++nb) {
+            tr[r][nb - 2] = 0.f;
+            if ((r == 0 && nb == 2) || (r == 1 && nb == 4)) continue;
+            g_node_rows = r ? 128 : 64;
+            g_node_blocks = nb;
+            tr[r][nb - 2] = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+          }
+        // bit-identity of the 64-row tiling against the 128-row one
+        const size_t nc = (size_t)M * N;
+        std::vector<float> c64(nc), c128(nc);
+        g_node_rows = 64; g_node_blocks = 3;
+        CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c64.data(), C, nc * 4, hipMemcpyDeviceToHost));
+        g_node_rows = 128; g_node_blocks = 2;
+        CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c128.data(), C, nc * 4, hipMemcpyDeviceToHost));
+        g_node_rows = 0; g_node_blocks = 0;
+        printf("M=%ld N=%d K=%d: default %.2f us (no bias/act %.2f us) | 128 rows: 2 blocks/CU %.2f, 3 %.2f | "
+               "64 rows: 3 blocks/CU %.2f, 4 %.2f us | 64-row bit-identical: %s\n", M, N, k, t * 1e3, t0 * 1e3,
+               tr[1][0] * 1e3, tr[1][1] * 1e3, tr[0][1] * 1e3, tr[0][2] * 1e3, c64 == c128 ? "yes" : "NO");
       }
     float te = time_it(50, s, [&] { hipLaunchKernelGGL(k_empty, dim3(160), dim3(256), 0, s); });
     printf("empty kernel, 160 blocks: %.2f us per launch\n", te * 1e3);

@@ -3,10 +3,13 @@
 // Pattern "rows": each store instruction writes 16 B per lane into 32 rows of 2 KB (two lanes per
 // row, 32 B per 128-B line), as edge layer 1's epilogue does. Pattern "lines": each instruction
 // writes 1 KB contiguous (8 whole lines). Targets: a 3.36 GB buffer (HBM) and a 16 MB buffer that
-// every block rewrites (L2-resident). One 512-thread block per CU, 256 KB per block per pass.
+// every block rewrites (L2-resident), and (`tools/store_bench sweep`) targets of 32-512 MB that the
+// same 3.36 GB of stores cycle through (Infinity-Cache-sized). One 512-thread block per CU, 256 KB
+// per block per pass.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <initializer_list>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -45,7 +48,8 @@ __global__ __launch_bounds__(512) void k_store(char* __restrict__ out, long ntil
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool sweep = argc > 1;
   const long big = 3360L << 20, small = 16L << 20;
   char* buf;
   CK(hipMalloc(&buf, big));
@@ -54,7 +58,8 @@ int main() {
   CK(hipEventCreate(&e1));
   for (int pass = 0; pass < 2; ++pass)
     for (int rows = 1; rows >= 0; --rows)
-      for (long sz : {big, small}) {
+      for (long sz : sweep ? std::initializer_list<long>{big, 512L << 20, 256L << 20, 192L << 20, 128L << 20, 64L << 20, 32L << 20, small}
+                           : std::initializer_list<long>{big, small}) {
         const long ntiles = sz / (256L * 2048);
         const long blocks = 2 * (big / (256L * 2048));  // same bytes written in every case
         auto launch = [&] {
@@ -73,8 +78,8 @@ int main() {
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= 5;
         if (pass == 1)
-          printf("%-5s pattern, %-4s target: %.3f ms for %.2f GB = %.2f TB/s\n", rows ? "rows" : "lines",
-                 sz == big ? "HBM" : "L2", ms, big / 1e9, big / (ms * 1e-3) / 1e12);
+          printf("%-5s pattern, %5ld MB target: %.3f ms for %.2f GB = %.2f TB/s\n", rows ? "rows" : "lines",
+                 sz >> 20, ms, big / 1e9, big / (ms * 1e-3) / 1e12);
       }
   return 0;
 }
