@@ -69,6 +69,14 @@ struct EdgeArgs {
   const int* node_n;             // EPI_SEGMEAN: atom count of each node's crystal
   float* agg;
   unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
+  // EPI_SEGMEAN on row tiles (k_edge16, fc batches): tile t = edge rows [256 t, 256 t + 256) of each
+  // conditioning, nodes cut at tile ends (ntiles = row tiles). rtiles[t] = {first node starting in
+  // the tile, first node starting after it, the node continued from tile t-1 or -1, its rows' offset
+  // in msgbuf}. A cut node's sum stays one sequential sum over its edges: tile t-1 publishes the
+  // partial sum of its head part (sbuf [P][ntiles][H]), tile t continues it (rcnt [P][ntiles][8]:
+  // one counter per column group of 64; msgbuf [P][r2tot][H]: the continued rows, written only when
+  // tile t-1 has not published in time). null rtiles = node tiles (tiles / ntiles).
+  const int4* rtiles; float* sbuf; float* msgbuf; unsigned* rcnt; long r2tot;
   // k_edge16_tail: per layer-1 row tile from flag_row0 on, the count of its finished column tiles
   // (EPI_EDGE bumps, EPI_SEGMEAN tiles reading rows >= flag_row0 wait); null = no intra-grid waits.
   // zero_flags / nzero: an EPI_EDGE launch's block 0 clears them for the next grid.
@@ -78,7 +86,8 @@ struct EdgeArgs {
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
             // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
-            // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN)
+            // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN); bit 6 (tests, exact
+            // results) = row tiles never wait for the previous tile's partial sums (msgbuf path)
 };
 // knn (radius-graph) edges, knn.hip: per-crystal scratch at cand_off[b] (n^2 * 27 entries; the final
 // list at 2 * cand_off[b]), outputs sorted by source node into ei / ej / fd at node_estart

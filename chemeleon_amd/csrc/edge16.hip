@@ -43,6 +43,17 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Cross-tile exchange of the row-tile segment sums (tiles of one grid on different XCDs): the
+// partial sums and continued rows are stored and loaded as agent-scope atomics (sc1: written through
+// to memory, read past the XCD's L2), ordered by s_waitcnt around the counter. No agent-scope fences:
+// those write back / invalidate the whole L2 of the XCD (measured: edge layer 2 +20%).
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 // one output tile: virtual block vb of nvb (the XCD-aware remap turns it into a tile index)
@@ -58,14 +69,22 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   long row0, nrows;
   int seg_c = 0;
   int2 seg = {0, 0};
+  long rtile = 0;  // row-tile mode: the tile index
   if (EPI == EPI_SEGMEAN) {
     const long rest = bid / ntn;
     seg_c = (int)(rest % g.npairs);
-    seg = g.tiles[rest / g.npairs];
-    const long es0 = g.node_estart[seg.x];
-    const long es1 = (seg.y < g.nnodes) ? g.node_estart[seg.y] : g.E;
-    row0 = (long)seg_c * g.E + es0;
-    nrows = es1 - es0;
+    if (g.rtiles) {  // edge rows [256 t, 256 t + 256) of conditioning seg_c, nodes cut at the tile ends
+      rtile = rest / g.npairs;
+      const long e0 = rtile * BM;
+      row0 = (long)seg_c * g.E + e0;
+      nrows = g.E - e0 < BM ? g.E - e0 : BM;
+    } else {
+      seg = g.tiles[rest / g.npairs];
+      const long es0 = g.node_estart[seg.x];
+      const long es1 = (seg.y < g.nnodes) ? g.node_estart[seg.y] : g.E;
+      row0 = (long)seg_c * g.E + es0;
+      nrows = es1 - es0;
+    }
   } else {
     row0 = g.row_base + (bid / ntn) * BM;
     nrows = g.M - row0 < BM ? g.M - row0 : BM;
@@ -517,18 +536,38 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     // of the waves writes its 128 columns to an LDS tile [256][132], then every thread sums node
     // segments of one column in edge order (scatter_add's order) — as k_edge_gemm.
     float* T = reinterpret_cast<float*>(lds);
+    // node list: {node, rows in this tile | first row in the tile << 10 | kind << 20}; kind 0 = a whole
+    // node, 1 = the head part of a node cut at the tile end (row tiles: listed first), 2 = the rest of a
+    // node begun in the previous tile (listed last)
     int2* info = reinterpret_cast<int2*>(lds + SEG_B);
-    const int nn = seg.y - seg.x;
+    int nn;
     int2 my = {0, 0};
-    {
+    if (g.rtiles) {
+      const int4 rt = g.rtiles[rtile];
+      const long e0 = rtile * BM, e1 = e0 + nrows;
+      const int nreg = rt.y - rt.x;
+      const bool head = nreg > 0 && g.node_estart[rt.y - 1] + g.node_n[rt.y - 1] > e1;
+      const bool cont = rt.z >= 0;
+      nn = nreg + (cont ? 1 : 0);
+      if (tid < nn) {
+        if (cont && tid == nn - 1) {
+          my.x = rt.z;
+          my.y = (int)(g.node_estart[rt.z] + g.node_n[rt.z] - e0) | (2 << 20);
+        } else {
+          my.x = rt.x + (head ? (tid == 0 ? nreg - 1 : tid - 1) : tid);
+          const long es = g.node_estart[my.x], end = es + g.node_n[my.x];
+          my.y = (int)((end > e1 ? e1 : end) - es) | ((int)(es - e0) << 10) | ((head && tid == 0) ? 1 << 20 : 0);
+        }
+      }
+    } else {
+      nn = seg.y - seg.x;
       const long es0 = g.node_estart[seg.x];
       if (tid < nn) {
-        const int nd = seg.x + tid;
-        my.x = g.node_n[nd];
-        my.y = (int)(g.node_estart[nd] - es0);
+        my.x = seg.x + tid;
+        my.y = g.node_n[my.x] | ((int)(g.node_estart[my.x] - es0) << 10);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
+    __builtin_amdgcn_sched_barrier(0);
     // scale undo + bias + SiLU per column group; the next group's scale / bias loads are issued
     // ahead of the current group's math (pinned there, else all 16 loads are hoisted and spill)
     f32x4 scv[2], bbv[2];
@@ -571,26 +610,86 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int col = tid & 127;
-      for (int k = tid >> 7; k < nn && !(g.dbg & 32); k += 4) {  // (dbg 32: profiling, no sums)
-        const int2 ni = info[k];
-        const float* src = T + ni.y * SEG_TP + col;
-        float sacc = 0.f;
-        int jj = 0;
-        for (; jj + 8 <= ni.x; jj += 8) {
-          float v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = src[(jj + u) * SEG_TP];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) sacc += v[u];
-        }
-        for (; jj < ni.x; ++jj) sacc += src[jj * SEG_TP];
-        const float mean = sacc / (float)(ni.x < 1 ? 1 : ni.x);
-        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + seg.x + k) * H + n0 + half * 128 + col] = mean;
-        if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it (a wave = one node)
+      const int gcol = n0 + half * 128 + col;
+      // the mean of a node over this wave's 64 columns (a wave = one node)
+      auto finish = [&](int node, float sacc, int cnt) __attribute__((always_inline)) {
+        const float mean = sacc / (float)(cnt < 1 ? 1 : cnt);
+        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + node) * H + gcol] = mean;
+        if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it
           float m = fabsf(mean);
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-          if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + seg.x + k, __float_as_uint(m));
+          if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + node, __float_as_uint(m));
+        }
+      };
+      // row tiles: one counter per (conditioning, boundary tile, column group of 64)
+      const int cidx = (n0 / BN) * 4 + half * 2 + (col >> 6);
+      for (int k = tid >> 7; k < nn && !(g.dbg & 32); k += 4) {  // (dbg 32: profiling, no sums)
+        const int2 nk = info[k];
+        const int4 ni = {nk.y & 1023, (nk.y >> 10) & 1023, nk.x, nk.y >> 20};  // {rows, first row, node, kind}
+        const float* src = T + ni.y * SEG_TP + col;
+        float sacc = 0.f;
+        bool own = true;  // this wave finishes the node
+        if (ni.w == 2) {
+          // The rest of a node begun in tile t-1, whose head wave publishes the partial sum of its rows
+          // (sbuf) and bumps the counter. Normally that has happened (tile t-1 was dispatched first and
+          // handles its head node first): continue the sum from it. Otherwise (bounded wait; tile t-1 may
+          // still be queued, e.g. on the previous XCD's share of the grid) leave these rows in msgbuf and
+          // bump the counter: whichever of the two arrives second finishes the node.
+          unsigned* cnt = g.rcnt + ((long)seg_c * g.ntiles + rtile) * 8 + cidx;
+          unsigned v = 0;
+          if (!(g.dbg & 64) && lane == 0) {
+            unsigned spins = 0;
+            while ((v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u && ++spins < 256u)
+              __builtin_amdgcn_s_sleep(2);
+          }
+          if (__builtin_amdgcn_readfirstlane(v) == 0u) {
+            float* mb = g.msgbuf + ((long)seg_c * g.r2tot + g.rtiles[rtile].w) * H + gcol;
+            for (int r = 0; r < ni.x; ++r) st_agent(mb + (long)r * H, src[r * SEG_TP]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (written through before the count)
+            unsigned old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            own = __builtin_amdgcn_readfirstlane(old) != 0u;
+          }
+          if (own) {
+            asm volatile("" ::: "memory");
+            sacc = ld_agent(g.sbuf + ((long)seg_c * g.ntiles + rtile) * H + gcol);
+            if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (next launch)
+          }
+        }
+        if (own) {
+          int jj = 0;
+          for (; jj + 8 <= ni.x; jj += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[(jj + u) * SEG_TP];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sacc += v[u];
+          }
+          for (; jj < ni.x; ++jj) sacc += src[jj * SEG_TP];
+        }
+        if (ni.w == 0) {
+          finish(ni.z, sacc, ni.x);
+        } else if (ni.w == 2) {
+          if (own) finish(ni.z, sacc, g.node_n[ni.z]);
+        } else {
+          // head part of a node cut at the tile end: publish the partial sum for tile t+1; if tile t+1
+          // has already left its rows in msgbuf, finish the node here
+          const long tb = rtile + 1;
+          unsigned* cnt = g.rcnt + ((long)seg_c * g.ntiles + tb) * 8 + cidx;
+          st_agent(g.sbuf + ((long)seg_c * g.ntiles + tb) * H + gcol, sacc);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (written through before the count)
+          unsigned old = 0;
+          if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__builtin_amdgcn_readfirstlane(old) != 0u) {
+            asm volatile("" ::: "memory");
+            if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int deg = g.node_n[ni.z];
+            const int r2 = deg - ni.x;  // the node's rows in tile t+1
+            const float* mb = g.msgbuf + ((long)seg_c * g.r2tot + g.rtiles[tb].w) * H + gcol;
+            for (int r = 0; r < r2; ++r) sacc += ld_agent(mb + (long)r * H);
+            finish(ni.z, sacc, deg);
+          }
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);  // everyone's tile reads are done before the next half is written
@@ -637,7 +736,8 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t 
       !g1.flags || g1.flags != g2.flags || g1.flag_row0 != g1.row_base || g2.flag_row0 != g1.row_base)
     return hipErrorInvalidValue;
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.tiles || g2.ntiles < 1 || !g2.agg || !g2.bias ||
-      !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale)
+      !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale ||
+      (g2.rtiles && (!g2.sbuf || !g2.msgbuf || !g2.rcnt || (long)g2.ntiles * BM < g2.E)))
     return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
@@ -659,6 +759,7 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
   long blocks;
   if (epi == EPI_SEGMEAN) {
     if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
+    if (g.rtiles && (!g.sbuf || !g.msgbuf || !g.rcnt || (long)g.ntiles * BM < g.E)) return hipErrorInvalidValue;
     blocks = (long)g.ntiles * g.npairs * (g.N / BN);
   } else {
     if (g.M <= g.row_base || g.row_base < 0) return hipErrorInvalidValue;

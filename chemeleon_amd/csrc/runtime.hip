@@ -66,6 +66,7 @@ struct chm_model {
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
+  int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int ncu = 0;           // compute units of the device the model lives on
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
@@ -84,6 +85,12 @@ struct chm_batch {
   int* node_n;  // atom count of each node's crystal
   int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
+  // fc batches: edge layer 2 (k_edge16) on row tiles of exactly 256 edge rows, nodes cut at the tile
+  // ends (EdgeArgs::rtiles); null for knn batches
+  int4* rtiles = nullptr;
+  long nrt = 0, r2tot = 0;  // row tiles; rows of the nodes continued from a previous tile
+  float *sbuf = nullptr, *msgbuf = nullptr;
+  unsigned* rcnt = nullptr;
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
@@ -268,6 +275,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (stg) m->edge_stagger = atoi(stg);
     const char* spl = getenv("CHM_EDGE_SPLIT");
     if (spl) m->edge_split = atoi(spl);
+    const char* rows = getenv("CHM_EDGE_ROWS");
+    if (rows) m->edge_rows = atoi(rows);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -374,6 +383,14 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge16 = value != 0;
     return CHM_OK;
   }
+  if (k == "edge_rows") {  // edge layer 2 on 256-row tiles (fc batches) or node-aligned tiles; bit-identical
+    m->edge_rows = value != 0;
+    return CHM_OK;
+  }
+  if (k == "edge_rows_nowait") {  // (tests) row tiles never wait for the previous tile: the msgbuf path
+    m->edge_dbg = value ? (m->edge_dbg | 64) : (m->edge_dbg & ~64);
+    return CHM_OK;
+  }
   return fail(CHM_E_ARG, "unknown option: " + k);
 }
 
@@ -407,6 +424,8 @@ struct BatchTables {
   std::vector<int> nat, noff, n2g, ei, ej, nn;
   std::vector<long> eoff, estart, coff;
   std::vector<int2> tiles;
+  std::vector<int4> rtiles;  // fc: row tiles of edge layer 2 (EdgeArgs::rtiles)
+  long nrt = 0, r2tot = 0;
   long N = 0, E = 0;  // knn: E = the edge capacity
   long C = 0;         // knn: candidate scratch entries (sum of n^2 * 27)
   bool knn = false;
@@ -439,6 +458,45 @@ static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t, const Ba
     if (t.E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
   }
   return CHM_OK;
+}
+
+// Row tiles of an fc batch (edge rows grouped by source node; node v's rows [estart, estart + n)):
+// tile t = rows [256 t, 256 t + 256), {first node starting in it, first node starting after it, the
+// node that began in tile t-1 and continues here (-1: none), the offset of those continued rows in
+// msgbuf}. Returns the continued rows' total (msgbuf rows per conditioning); out null: sizing only.
+static long row_tiles(const BatchTables& t, std::vector<int4>* out) {
+  const long E = t.E, nrt = (E + kTileRows - 1) / kTileRows;
+  if (out) out->assign(nrt, make_int4((int)t.N, (int)t.N, -1, 0));
+  long r2tot = 0, tc = 0, node = 0;
+  long prev_end = 0;  // end row of the previous node
+  for (size_t g = 0; g < t.nat.size(); ++g)
+    for (int i = 0; i < t.nat[g]; ++i, ++node) {
+      const long es = t.eoff[g] + (long)i * t.nat[g];
+      for (; tc < nrt && tc * kTileRows <= es; ++tc) {  // tiles starting in (previous start, es]
+        const long s0 = tc * kTileRows;
+        int4 r = make_int4((int)node, (int)t.N, -1, 0);
+        if (node > 0 && prev_end > s0 && s0 < es) {  // node-1 began before the tile and reaches into it
+          r.z = (int)(node - 1);
+          r.w = (int)r2tot;
+          r2tot += prev_end - s0;
+        }
+        if (out) (*out)[tc] = r;
+      }
+      prev_end = es + t.nat[g];
+    }
+  for (; tc < nrt; ++tc) {  // tiles after the last node start (the last node's rest)
+    const long s0 = tc * kTileRows;
+    int4 r = make_int4((int)t.N, (int)t.N, -1, 0);
+    if (prev_end > s0) {
+      r.z = (int)(t.N - 1);
+      r.w = (int)r2tot;
+      r2tot += prev_end - s0;
+    }
+    if (out) (*out)[tc] = r;
+  }
+  if (out)
+    for (long k = 0; k < nrt; ++k) (*out)[k].y = k + 1 < nrt ? (*out)[k + 1].x : (int)t.N;
+  return r2tot;
 }
 
 // fills the per-node / per-edge tables (only when the batch is really built)
@@ -480,6 +538,8 @@ static void batch_fill(BatchTables& t) {
       rows += t.nat[g];
     }
   t.tiles.push_back(make_int2(cur0, (int)N));
+  t.r2tot = row_tiles(t, &t.rtiles);
+  t.nrt = (long)t.rtiles.size();
 }
 
 // number of segment tiles without building the tables (sizing only)
@@ -517,6 +577,12 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->node_estart = (long*)carve(N * sizeof(long));
   b->node_n = (int*)carve(N * sizeof(int));
   b->tiles = (int2*)carve(ntiles * sizeof(int2));
+  if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
+    b->rtiles = (int4*)carve(b->nrt * sizeof(int4));
+    b->sbuf = fl((size_t)P * b->nrt * H);
+    b->msgbuf = fl((size_t)P * (b->r2tot + 1) * H);
+    b->rcnt = (unsigned*)carve((size_t)P * b->nrt * 8 * sizeof(unsigned));
+  }
   if (b->knn) {  // (E = the edge capacity E_cap)
     b->cand_off = (long*)carve((B + 1) * sizeof(long));
     b->cand_key = (unsigned*)carve(b->C_cap * sizeof(unsigned));
@@ -575,6 +641,8 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->E_cap = t.E;
   b->C_cap = t.C;
   b->ntiles = t.knn ? (int)(t.N + 1) : (int)t.tiles.size();
+  b->nrt = t.knn ? 0 : t.nrt;
+  b->r2tot = t.knn ? 0 : t.r2tot;
   const size_t need = batch_layout(b, m, nullptr, b->ntiles);
   char* base = (char*)d_ws;
   if (!base) {
@@ -623,6 +691,9 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->node_estart, t.estart.data(), t.N * sizeof(long));
     up(b->node_n, t.nn.data(), t.N * sizeof(int));
     up(b->tiles, t.tiles.data(), t.tiles.size() * sizeof(int2));
+    up(b->rtiles, t.rtiles.data(), t.rtiles.size() * sizeof(int4));
+    if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
+      e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
@@ -656,6 +727,10 @@ extern "C" size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t
   b.E = t.E;
   b.knn = bo.knn;
   b.C_cap = t.C;
+  if (!t.knn) {
+    b.nrt = (t.E + kTileRows - 1) / kTileRows;
+    b.r2tot = row_tiles(t, nullptr);
+  }
   return batch_layout(&b, m, nullptr, count_tiles(t));
 }
 
@@ -839,7 +914,7 @@ static int knn_build(chm_batch* b, const float* x, const float* lat, hipStream_t
     if (d > kTileRows) return fail(CHM_E_UNSUPPORTED, "knn: a node with more than 256 edges");
     b->h_estart[v] = E;
     E += d;
-    if (rows + d > kTileRows) {
+    if (rows + d > kTileRows || v - cur0 >= kTileRows) {  // (<= 256 nodes: isolated atoms add no rows)
       b->h_tiles.push_back(make_int2(cur0, (int)v));
       cur0 = (int)v;
       rows = 0;
@@ -935,6 +1010,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       e2.node_estart = b->node_estart; e2.natoms = b->natoms; e2.n2g = b->n2g; e2.agg = b->agg;
       e2.node_n = b->node_n; e2.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
       e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
+      if (m->edge16 && m->edge_rows && b->rtiles) {  // 256-row tiles, cut nodes continued across tiles
+        e2.rtiles = b->rtiles; e2.ntiles = (int)b->nrt; e2.sbuf = b->sbuf; e2.msgbuf = b->msgbuf;
+        e2.rcnt = b->rcnt; e2.r2tot = b->r2tot;
+      }
       // (instrumented eager launches keep one launch per layer, so the per-kernel timings stay whole;
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;

@@ -262,6 +262,36 @@ def test_edge_tail_split_is_bit_identical(cn, nat):
         assert torch.equal(u, v), f"{what}: split and one-launch-per-layer edge schedules differ"
 
 
+@pytest.mark.parametrize("nat", [[40] * 64, [20] * 48, [80] * 9, [1] * 300 + [2] * 70 + [3] * 9,
+                                 [23, 7, 40, 1, 80] * 23, [5, 9, 3, 12, 7, 1, 20]])
+def test_edge_row_tiles_are_bit_identical(cn, nat):
+    """Edge layer 2 on row tiles of exactly 256 edge rows (default; option 'edge_rows'): a node cut at
+    a tile end keeps one sequential sum over its edges (the previous tile publishes its partial sum,
+    the next continues it, or finishes it from the continued rows left in msgbuf when the partial was
+    not there in time). One reverse step must agree bit for bit with node-aligned segment tiles, with
+    the waiting path and with the msgbuf path forced ('edge_rows_nowait'). Shapes: 64 x 40 (with the
+    layer-1 tail split), crystals of 20 and 80 atoms, runs of 1-3-atom crystals (up to 256 nodes per
+    tile), ragged 1-80, a small mixed batch."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(12)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    outs = []
+    for rows, nowait in ((0, 0), (1, 0), (1, 1), (1, 0)):
+        model.decoder.set_option("edge_rows", rows)
+        model.decoder.set_option("edge_rows_nowait", nowait)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+    del model
+    torch.cuda.empty_cache()
+    for k, name in ((1, "row tiles"), (2, "row tiles, msgbuf path"), (3, "row tiles, second run")):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: {name} differ from node-aligned segment tiles"
+
+
 @pytest.mark.parametrize("tag", ["64x20", "16x40"])
 def test_teacher_forced_steps_edge32_kernels(golden, cn, tag):
     """The round-1 split16 edge kernels (v_mfma_f32_32x32x16_f16, k_edge_gemm; option edge16 = 0)
