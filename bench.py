@@ -293,6 +293,21 @@ def main():
         for _ in it2:
             pass
         torch.cuda.synchronize()
+    # the dominant kernel: both edge layers in one grid (k_edge16_layer, the default on fc batches) or,
+    # when that is off, the edge message GEMM; with the one-grid kernel on, a second eager pass times the
+    # two layers as separate launches for context
+    nlay, ms_lay = _lib.prof_read(_lib.K_EDGE_LAYER)
+    ndec, ms_dec = _lib.prof_read(_lib.K_DECODER)
+    if nlay:
+        _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
+        model.decoder.set_option("edge_layer", 0)
+        it3 = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
+                                  null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
+                                  init=init, t_stop=998, graph=False)
+        for _ in it3:
+            pass
+        torch.cuda.synchronize()
+        model.decoder.set_option("edge_layer", 1)
     _lib.check(_lib.load().chm_prof_enable(0), "prof_disable")
     if dist is not None:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -308,7 +323,6 @@ def main():
     # live per-kernel timing (HIP events on the launch stream)
     nmsg, ms_msg = _lib.prof_read(_lib.K_EDGE_MESSAGE)
     nfou, ms_fou = _lib.prof_read(_lib.K_EDGE_FOURIER)
-    ndec, ms_dec = _lib.prof_read(_lib.K_DECODER)
     E = sum(n * n for n in natoms)
     N = sum(natoms)
     msg_flops = 2.0 * (2 * E) * H * H  # one launch covers both conditionings
@@ -319,9 +333,11 @@ def main():
     fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
     edge16 = os.environ.get("CHM_EDGE16", "1") != "0"
-    msg_kernel = "k_edge16<2" if edge16 else "k_edge_gemm<2"
+    msg_kernel = "k_edge16_layer" if nlay else ("k_edge16<2" if edge16 else "k_edge_gemm<2")
     traffic, traffic_src = (_pmc_traffic(math, msg_kernel) if not args.ragged else
                             (None, "not collected for the ragged workload"))
+    lay_flops = fou_flops + msg_flops
+    lay_tflops = lay_flops / (ms_lay / nlay * 1e-3) / 1e12 if nlay else None
     # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
     # = bf16 rate) / 3 products; f32 = the fp32 MFMA peak
     peak = {"bf16x3": BF16X3_PEAK_TFLOPS, "split16": MFMA_BF16_PEAK_TFLOPS / 3}.get(math, MFMA_F32_PEAK_TFLOPS)
@@ -374,20 +390,25 @@ def main():
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
-                     "kernel": {"split16": f"edge message GEMM + fused scatter_mean ({msg_kernel}, EPI_SEGMEAN, "
-                                           f"{'16x16x32' if edge16 else '32x32x16'} MFMA), both conditionings",
+                     "kernel": {"split16": ("both edge layers of a CSP layer in one grid (k_edge16_layer: D.f + P_i + "
+                                            "Q_j + SiLU -> S, S.W2^T + SiLU + fused scatter_mean; 16x16x32 MFMA), "
+                                            "both conditionings, incl. its two repair launches (no-ops unless a "
+                                            "check fails)") if nlay else
+                                           (f"edge message GEMM + fused scatter_mean ({msg_kernel}, EPI_SEGMEAN, "
+                                            f"{'16x16x32' if edge16 else '32x32x16'} MFMA), both conditionings"),
                                 "bf16x3": "edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), "
                                           "both conditionings",
                                 "f32": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"}[math],
-                     "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
-                     "frac": (msg_tflops / peak) if msg_tflops else None, "traffic": traffic,
+                     "achieved": lay_tflops if nlay else msg_tflops, "peak": peak, "unit": "TFLOP/s",
+                     "frac": ((lay_tflops if nlay else msg_tflops) / peak) if (lay_tflops or msg_tflops) else None,
+                     "traffic": traffic,
                      "traffic_source": traffic_src,
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
                                    "split16": "fp32-equivalent flops (3 fp16 MFMA products each); fp16 dense MFMA "
                                            "2.5 PF / 3 products",
                                    "f32": "fp32 MFMA dense peak"}[math],
-                     "flops_per_launch": msg_flops, "launches": nmsg,
-                     "avg_ms": ms_msg / nmsg if nmsg else None},
+                     "flops_per_launch": lay_flops if nlay else msg_flops, "launches": nlay or nmsg,
+                     "avg_ms": (ms_lay / nlay) if nlay else (ms_msg / nmsg if nmsg else None)},
         "msgpass": {"bound": "hbm", "kernel": "k_segment_mean (standalone scatter_mean, chm_segment_mean)",
                     "achieved": seg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": (seg_gbs / HBM_PEAK_GBS) if seg_gbs else None, "bytes_per_launch": seg_bytes,
@@ -395,6 +416,11 @@ def main():
                     "note": ("in the sampler the aggregation is fused into the message GEMM epilogue; this is the "
                              "standalone kernel on the same [2,E,512] shape" if math != "f32" else
                              "the kernel as launched by the sampler")},
+        "edge_layer2": {"kernel": "edge layer 2 alone (k_edge16<2>: S.W2^T + SiLU + fused scatter_mean), both "
+                                  "conditionings" + (" (second eager pass, two launches per layer)" if nlay else ""),
+                        "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
+                        "frac": (msg_tflops / peak) if msg_tflops else None, "flops_per_launch": msg_flops,
+                        "avg_ms": ms_msg / nmsg if nmsg else None},
         "edge_layer1": {"kernel": "edge layer 1 (D.f + P_i + Q_j + SiLU, S written split), both conditionings",
                         "achieved": fou_tflops, "peak": peak, "unit": "TFLOP/s",
                         "frac": (fou_tflops / peak) if fou_tflops else None, "flops_per_launch": fou_flops,

@@ -144,7 +144,7 @@ def require_device(*tensors):
 
 
 MATH_BF16X3, MATH_F32, MATH_SPLIT16 = 0, 1, 2
-K_EDGE_FOURIER, K_EDGE_MESSAGE, K_SEGMENT_MEAN, K_DECODER = 0, 1, 2, 3
+K_EDGE_FOURIER, K_EDGE_MESSAGE, K_SEGMENT_MEAN, K_DECODER, K_EDGE_LAYER = 0, 1, 2, 3, 4
 
 
 def prof_read(kernel: int):

@@ -40,6 +40,7 @@ struct GemmArgs {
   const long* node_estart;                // first edge row of each node
   const int* natoms; const int* n2g;
   float* agg;                             // [P][N][H]
+  int linear_order;                       // node_gemm: 1 = tiles in launch order (A/B only), 0 = XCD-aware
 };
 
 enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
@@ -77,6 +78,10 @@ struct EdgeArgs {
   // one counter per column group of 64; msgbuf [P][r2tot][H]: the continued rows, written only when
   // tile t-1 has not published in time). null rtiles = node tiles (tiles / ntiles).
   const int4* rtiles; float* sbuf; float* msgbuf; unsigned* rcnt; long r2tot;
+  // k_edge16_layer (both edge layers in one grid): per row tile, the count of layer-1 column tiles that
+  // have written S through, then of the layer-2 tiles that have read it (the last one resets it to 0)
+  unsigned* lflags;
+  unsigned* xbad;  // k_edge16_layer: raised by a layer-2 tile that read S of another XCD (repair needed)
   // k_edge16_tail: per layer-1 row tile from flag_row0 on, the count of its finished column tiles
   // (EPI_EDGE bumps, EPI_SEGMEAN tiles reading rows >= flag_row0 wait); null = no intra-grid waits.
   // zero_flags / nzero: an EPI_EDGE launch's block 0 clears them for the next grid.
@@ -87,7 +92,8 @@ struct EdgeArgs {
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
             // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
             // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN); bit 6 (tests, exact
-            // results) = row tiles never wait for the previous tile's partial sums (msgbuf path)
+            // results) = row tiles never wait for the previous tile's partial sums (msgbuf path); bit 9
+            // (tests, exact results) = k_edge16_layer's layer-2 tiles always request the repair launches
 };
 // knn (radius-graph) edges, knn.hip: per-crystal scratch at cand_off[b] (n^2 * 27 entries; the final
 // list at 2 * cand_off[b]), outputs sorted by source node into ei / ej / fd at node_estart
@@ -123,6 +129,8 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
 // one grid: edge layer 1 (EPI_EDGE, g1: a row range) first, then edge layer 2 (EPI_SEGMEAN, g2: segment
 // tiles that read none of g1's rows)
 hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s);
+// both edge layers in one grid (row tiles; layer-2 tiles of row tile i - lag behind layer 1's row tile i)
+hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s);
 hipError_t edge16_init();
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,

@@ -53,18 +53,29 @@ __device__ __forceinline__ void st_agent(float* p, float v) {
 __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the XCD (XCC) this wave runs on
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
 
 }  // namespace
 
-// one output tile: virtual block vb of nvb (the XCD-aware remap turns it into a tile index)
-template <int EPI, bool ASC>
-__device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb) {
+// one output tile: virtual block vb of nvb (the XCD-aware remap turns it into a tile index), or the
+// tile index itself (bid_in >= 0). ONE (k_edge16_layer, both edge layers in one grid): layer-2 tiles
+// wait for the layer-1 tiles of their rows (EdgeArgs::lflags) and read S through the XCD's L2, which
+// is coherent only if those layer-1 tiles ran on the same XCD: the layer-1 tiles record their XCD in
+// the flag word and a layer-2 tile that finds another one raises *xbad (the runtime's repair launches
+// then recompute the layer).
+template <int EPI, bool ASC, bool ONE = false>
+__device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb, long bid_in = -1) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int l16 = lane & 15, g4 = lane >> 4;
   const int ntn = g.N / BN;
-  const long bid = remap(vb, nvb);
+  const long bid = bid_in >= 0 ? bid_in : remap(vb, nvb);
   const int n0 = (int)(bid % ntn) * BN;
   long row0, nrows;
   int seg_c = 0;
@@ -157,13 +168,35 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     }
   }
 
+  if constexpr (ONE && EPI == EPI_SEGMEAN) {
+    // k_edge16_layer: wait (bounded) until both layer-1 column tiles of these rows have stored S and
+    // its exponents (flag word: count in bits 0-7, each layer-1 tile's XCD + 1 in bits 8 + 4 n0), check
+    // that they ran on this XCD, then count this tile as a consumer (the last of the 2 P resets it)
+    if (tid == 0) {
+      unsigned* f = g.lflags + rtile;
+      const unsigned need = (unsigned)(g.N / BN);
+      unsigned spins = 0, v;
+      while (((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffu) < need &&
+             ++spins < (1u << 21))
+        __builtin_amdgcn_s_sleep(4);
+      const unsigned me = xcc_id() + 1u;
+      if (((v >> 8) & 15u) != me || ((v >> 12) & 15u) != me || (v & 0xffu) < need || (g.dbg & 512))
+        __hip_atomic_store(g.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned last = need + 2u * (unsigned)g.npairs - 1u;
+      if ((__hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffu) == last)
+        __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+
   // ---- row exponents of the A chunks (edge layer 2): the lane's four rows
   int ex[4] = {0, 0, 0, 0};
   if (ASC) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const long lr = wm * 64 + 16 * i + l16;
-      ex[i] = g.aexp[row0 + (lr < nrows ? lr : nrows - 1)];
+      const int* pe = g.aexp + row0 + (lr < nrows ? lr : nrows - 1);
+      ex[i] = *pe;
     }
   }
 
@@ -493,8 +526,10 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           if (st_e) *reinterpret_cast<f16x8*>(se + cc * 64) = odd ? r8 : hv;  // row 2p: hi (even), lo (odd)
           if (st_o) *reinterpret_cast<f16x8*>(so + cc * 64) = odd ? lv : r8;  // row 2p+1
         }
-        if (lr < nrows && !nostore && g4 == 0)
-          reinterpret_cast<signed char*>(g.sexp)[orow * 4 + (n0 + wn * 128) / CHUNK] = (signed char)ex2;
+        if (lr < nrows && !nostore && g4 == 0) {
+          signed char* pe = reinterpret_cast<signed char*>(g.sexp) + orow * 4 + (n0 + wn * 128) / CHUNK;
+          *pe = (signed char)ex2;
+        }
       });
     };
     using F = std::integral_constant<bool, false>;
@@ -516,6 +551,15 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       all(Tr{});
     else
       all(F{});
+    if constexpr (ONE) {
+      // k_edge16_layer: every store of this tile has reached the XCD's L2; count the column tile and
+      // record this XCD for the layer-2 tiles' check
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add(g.lflags + (row0 / BM), 1u + ((xcc_id() + 1u) << (8 + 4 * (n0 / BN))), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (g.flags) {
       // k_edge16_tail: publish this tile (S rows + exponents) to the segment tiles of the same grid
       // that read it: every wave's stores have reached L2, one agent-scope release writes the XCD's
@@ -719,10 +763,62 @@ __global__ __launch_bounds__(512, 1) void k_edge16_tail(EdgeArgs g1, EdgeArgs g2
   }
 }
 
+// Both edge layers of a CSP layer in one grid (fc batches on row tiles): every XCD (blockIdx % 8) walks
+// its own contiguous range of row tiles, layer-1 tiles (2 column tiles) of row tile i interleaved with
+// the layer-2 tiles (P conditionings x 2 column tiles) of row tile i - D, so a layer-2 tile normally
+// starts after the layer-1 tiles it reads have finished, and the two layers' phases (layer 1's
+// epilogue store bursts, layer 2's MFMA-bound main loop) overlap across the CUs instead of every CU
+// storing at once. Dependencies only point to earlier blocks of the same XCD's sequence (dispatched
+// in index order), and the waits are bounded.
+__global__ __launch_bounds__(512, 1) void k_edge16_layer(EdgeArgs g1, EdgeArgs g2, int R, int D) {
+  const int x = blockIdx.x & 7;
+  const long k = blockIdx.x >> 3;
+  const long lo = (long)R * x / 8, hi = (long)R * (x + 1) / 8, n = hi - lo;
+  const int P = g2.npairs, G = 2 + 2 * P;
+  const long d = D < n ? D : n;
+  long i;
+  int s;
+  if (k < 2 * d) {
+    i = k / 2;
+    s = (int)(k % 2);
+  } else if (k - 2 * d < (n - d) * G) {
+    i = d + (k - 2 * d) / G;
+    s = (int)((k - 2 * d) % G);
+  } else {
+    const long k2 = k - 2 * d - (n - d) * G;
+    if (k2 >= d * 2 * P) return;
+    i = n + k2 / (2 * P);
+    s = 2 + (int)(k2 % (2 * P));
+  }
+  if (s < 2)
+    edge16_tile<EPI_EDGE, false, true>(g1, blockIdx.x, gridDim.x, (lo + i) * 2 + s);
+  else
+    edge16_tile<EPI_SEGMEAN, true, true>(g2, blockIdx.x, gridDim.x, ((lo + i - d) * P + (s - 2) / 2) * 2 + (s - 2) % 2);
+}
+
+// Repair of a k_edge16_layer launch whose check failed (*g.xbad != 0: some layer-2 tile read S written
+// on another XCD, so its L2 view may have been stale): one layer on the two-launch schedule, grid-
+// stride over the tiles so that the normal case (nothing to repair) costs one small grid that exits.
+// The layer-1 pass also clears the layer's agg row maxima (the failed launch may have max-ed garbage).
+template <int EPI, bool ASC>
+__global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, unsigned* agg_max, long nmax,
+                                                          unsigned* lflags, long nrt) {
+  if (__hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  if (EPI == EPI_EDGE && agg_max) {  // (and the row-tile flags, in case a wait timed out)
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrt; k += (long)gridDim.x * 512) lflags[k] = 0u;
+  }
+  for (long vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    edge16_tile<EPI, ASC>(g, vb, nvb);
+    __syncthreads();
+  }
+}
+
 hipError_t edge16_init() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
-                      (const void*)k_edge16_tail};
+                      (const void*)k_edge16_tail, (const void*)k_edge16_layer,
+                      (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
@@ -749,6 +845,39 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t 
   const long nb1 = (nt1 + 7) / 8 * 8;
   const long nt2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
   hipLaunchKernelGGL(k_edge16_tail, dim3((unsigned)(nb1 + nt2)), dim3(512), LDS_B, s, g1, g2, (int)nb1, (int)nt1);
+  return hipGetLastError();
+}
+
+hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s) {
+  if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
+      !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.row_base != 0 || g1.flags || !g1.lflags ||
+      !g1.xbad || g1.xbad != g2.xbad)
+    return hipErrorInvalidValue;
+  if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.rtiles || !g2.sbuf || !g2.msgbuf || !g2.rcnt || !g2.agg ||
+      !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags != g1.lflags ||
+      g2.npairs != g1.npairs || (long)g2.ntiles * BM < g2.E || (long)g2.ntiles * BM - g2.E >= BM || g1.M != g1.E ||
+      lag < 1)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = edge16_init();
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long R = g2.ntiles, nmax = (R + 7) / 8;
+  const long blocks = 8 * nmax * (2 + 2L * g2.npairs);
+  hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // the repair pair (exits at once unless a layer-2 tile flagged another XCD's layer-1 tile)
+  EdgeArgs r1 = g1, r2 = g2;
+  r1.lflags = r2.lflags = nullptr;
+  const long nb1 = ((g1.M + BM - 1) / BM) * (g1.N / BN), nb2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
+  const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
+  hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, nb1, g2.agg_max,
+                     (long)g2.npairs * g2.nnodes, g1.lflags, R);
+  hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nb2, (unsigned*)nullptr, 0L,
+                     (unsigned*)nullptr, 0L);
   return hipGetLastError();
 }
 

@@ -60,6 +60,11 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+__device__ __forceinline__ long xcd_remap(long b, long nb) {
+  const long q = nb / 8, r = nb % 8, xcd = b % 8, idx = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 __device__ __forceinline__ float silu_n(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
@@ -88,7 +93,10 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
   const int ntn = g.N / NN;
-  const long bid = blockIdx.x;
+  // XCD-aware order (workgroups go round-robin to the 8 XCDs): each XCD takes a contiguous range of
+  // tiles, so the column tiles of a row tile run on one XCD and read their A rows once from HBM
+  // (without it every column tile fetched A again into another XCD's L2: 538 MB per launch vs 84-168)
+  const long bid = g.linear_order ? (long)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int n0 = (int)(bid % ntn) * NN;
   const long row0 = (bid / ntn) * NM;
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
@@ -361,7 +369,10 @@ int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
-hipError_t node_gemm(const GemmArgs& g, hipStream_t s) {
+hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
+  static const int linear = getenv("CHM_NODE_LINEAR") ? atoi(getenv("CHM_NODE_LINEAR")) : 0;  // (A/B only)
+  GemmArgs g = g_in;
+  g.linear_order = linear;
   if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
   if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
   static bool attr = false;

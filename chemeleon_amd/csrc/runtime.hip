@@ -67,6 +67,8 @@ struct chm_model {
   int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
+  int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
+  int edge_lag = 10;     // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD
   int ncu = 0;           // compute units of the device the model lives on
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
@@ -91,6 +93,8 @@ struct chm_batch {
   long nrt = 0, r2tot = 0;  // row tiles; rows of the nodes continued from a previous tile
   float *sbuf = nullptr, *msgbuf = nullptr;
   unsigned* rcnt = nullptr;
+  unsigned* lflags = nullptr;  // k_edge16_layer: per row tile (returns to 0 at the end of every launch)
+  unsigned* xbad = nullptr;    // k_edge16_layer: per layer, raised when its repair launches must run
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
@@ -277,6 +281,10 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (spl) m->edge_split = atoi(spl);
     const char* rows = getenv("CHM_EDGE_ROWS");
     if (rows) m->edge_rows = atoi(rows);
+    const char* lay = getenv("CHM_EDGE_LAYER");
+    if (lay) m->edge_layer = atoi(lay);
+    const char* lag = getenv("CHM_EDGE_LAG");
+    if (lag) m->edge_lag = atoi(lag) > 0 ? atoi(lag) : 1;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -385,6 +393,19 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
   }
   if (k == "edge_rows") {  // edge layer 2 on 256-row tiles (fc batches) or node-aligned tiles; bit-identical
     m->edge_rows = value != 0;
+    return CHM_OK;
+  }
+  if (k == "edge_layer") {  // both edge layers in one grid (fc batches, row tiles); bit-identical
+    m->edge_layer = value != 0;
+    return CHM_OK;
+  }
+  if (k == "edge_lag") {
+    if (value < 1 || value > 1000) return fail(CHM_E_ARG, "edge_lag must be in [1, 1000]");
+    m->edge_lag = (int)value;
+    return CHM_OK;
+  }
+  if (k == "edge_layer_repair") {  // (tests) k_edge16_layer always runs its repair launches
+    m->edge_dbg = value ? (m->edge_dbg | 512) : (m->edge_dbg & ~512);
     return CHM_OK;
   }
   if (k == "edge_rows_nowait") {  // (tests) row tiles never wait for the previous tile: the msgbuf path
@@ -582,6 +603,8 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->sbuf = fl((size_t)P * b->nrt * H);
     b->msgbuf = fl((size_t)P * (b->r2tot + 1) * H);
     b->rcnt = (unsigned*)carve((size_t)P * b->nrt * 8 * sizeof(unsigned));
+    b->lflags = (unsigned*)carve(b->nrt * sizeof(unsigned));
+    b->xbad = (unsigned*)carve(64 * sizeof(unsigned));
   }
   if (b->knn) {  // (E = the edge capacity E_cap)
     b->cand_off = (long*)carve((B + 1) * sizeof(long));
@@ -694,6 +717,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->rtiles, t.rtiles.data(), t.rtiles.size() * sizeof(int4));
     if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
+    if (e == hipSuccess && b->lflags) e = hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
@@ -972,6 +996,12 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     }
     HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
   }
+  if (b->xbad && m->edge16 && m->edge_rows && m->edge_layer && b->math == MATH_SPLIT16) {
+    // k_edge16_layer: repair requests and row-tile flags start clear in every call (the flags also
+    // return to 0 at the end of every launch; this keeps a timed-out wait from leaking into later calls)
+    HIPCHK(hipMemsetAsync(b->xbad, 0, 64 * sizeof(unsigned), s));
+    HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
+  }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
     if (m->film) {  // FiLM projection (cspnet.py:92)
@@ -1018,7 +1048,13 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !instrumented && !m->edge_trace) {
+      if (e2.rtiles && m->edge_layer && !m->edge_trace) {
+        // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
+        e1.lflags = e2.lflags = b->lflags;
+        e1.xbad = e2.xbad = b->xbad + l;
+        ProfScope ps(CHM_K_EDGE_LAYER, s);
+        HIPCHK(edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s));
+      } else if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !instrumented && !m->edge_trace) {
         // Edge layer 1 in whole rounds of the grid (rows [0, l1_rows_a)), then one grid with its
         // partial last round first and all of edge layer 2's segment tiles behind it (the few that
         // read those rows wait for them inside the grid). Same tiles, same arithmetic: bit-identical

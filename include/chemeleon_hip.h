@@ -282,11 +282,13 @@ int chm_edge_features_split(chm_batch* b, const float* d_frac, void* d_split, vo
  *   CHM_K_EDGE_FOURIER  edge layer 1 (Fourier projection + node terms + SiLU)
  *   CHM_K_EDGE_MESSAGE  edge layer 2 (message GEMM + SiLU)
  *   CHM_K_SEGMENT_MEAN  message-passing aggregation (scatter_mean)
- *   CHM_K_DECODER       one whole decoder call (all its kernels) */
+ *   CHM_K_DECODER       one whole decoder call (all its kernels)
+ *   CHM_K_EDGE_LAYER    both edge layers of a CSP layer in one grid (k_edge16_layer + its repair pair) */
 #define CHM_K_EDGE_FOURIER 0
 #define CHM_K_EDGE_MESSAGE 1
 #define CHM_K_SEGMENT_MEAN 2
 #define CHM_K_DECODER 3
+#define CHM_K_EDGE_LAYER 4
 int chm_prof_enable(int on);
 int chm_prof_reset(void);
 int chm_prof_read(int kernel, int64_t* launches, double* total_ms);

@@ -271,7 +271,10 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
     not there in time). One reverse step must agree bit for bit with node-aligned segment tiles, with
     the waiting path and with the msgbuf path forced ('edge_rows_nowait'). Shapes: 64 x 40 (with the
     layer-1 tail split), crystals of 20 and 80 atoms, runs of 1-3-atom crystals (up to 256 nodes per
-    tile), ragged 1-80, a small mixed batch."""
+    tile), ragged 1-80, a small mixed batch. The same for both edge layers in one grid (option
+    'edge_layer', k_edge16_layer: layer-2 row tiles wait for the layer-1 tiles of their rows and read S
+    through the XCD's L2) at lags of 10, 1 and 3 row tiles, and with its repair launches forced
+    ('edge_layer_repair': the layer recomputed on the two-launch schedule)."""
     B, N = len(nat), sum(nat)
     g = torch.Generator().manual_seed(12)
     a0 = torch.randint(0, 100, (N,), generator=g)
@@ -281,13 +284,19 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
           torch.randn(N, 3, generator=g))
     model = _model(1000)
     outs = []
-    for rows, nowait in ((0, 0), (1, 0), (1, 1), (1, 0)):
+    for rows, nowait, layer, lag, repair in ((0, 0, 0, 10, 0), (1, 0, 0, 10, 0), (1, 1, 0, 10, 0), (1, 0, 0, 10, 0),
+                                             (1, 0, 1, 10, 0), (1, 0, 1, 1, 0), (1, 1, 1, 3, 0), (1, 0, 1, 10, 1)):
         model.decoder.set_option("edge_rows", rows)
         model.decoder.set_option("edge_rows_nowait", nowait)
+        model.decoder.set_option("edge_layer", layer)
+        model.decoder.set_option("edge_lag", lag)
+        model.decoder.set_option("edge_layer_repair", repair)
         outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
     del model
     torch.cuda.empty_cache()
-    for k, name in ((1, "row tiles"), (2, "row tiles, msgbuf path"), (3, "row tiles, second run")):
+    for k, name in ((1, "row tiles"), (2, "row tiles, msgbuf path"), (3, "row tiles, second run"),
+                    (4, "both edge layers in one grid"), (5, "one grid, lag 1"), (6, "one grid, lag 3, msgbuf path"),
+                    (7, "one grid + forced repair launches")):
         for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
             assert torch.equal(u, v), f"{what}: {name} differ from node-aligned segment tiles"
 

@@ -4,7 +4,16 @@ import sys
 
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
 j = json.loads(line)
+r = j["roofline"]
+l2 = j.get("edge_layer2") or {}
+l1 = j.get("edge_layer1") or {}
+
+
+def f(v, fmt):
+    return format(v, fmt) if isinstance(v, (int, float)) else "-"
+
+
 print(f"{j['value']:.3f} {j['unit']}  {j['ms_per_step']:.2f} ms/step  "
-      f"L2 {j['roofline']['avg_ms']:.3f} ms ({j['roofline']['frac']:.3f})  "
-      f"L1 {j['edge_layer1']['avg_ms']:.3f} ms ({j['edge_layer1']['frac']:.3f})  "
+      f"dominant {f(r['avg_ms'], '.3f')} ms ({f(r['frac'], '.3f')})  "
+      f"L2 {f(l2.get('avg_ms'), '.3f')} ms  L1 {f(l1.get('avg_ms'), '.3f')} ms  "
       f"path {j['path']['tflops']:.0f} TF")
