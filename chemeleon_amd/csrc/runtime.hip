@@ -47,6 +47,9 @@ struct LayerW {
 enum MathMode { MATH_BF16X3 = 0, MATH_F32 = 1, MATH_SPLIT16 = 2 };
 constexpr long kTileRows = 256;  // rows of the edge-GEMM tiles (gemm_bf16x3_big)
 constexpr int kMaxTailTiles = 512;  // layer-1 row tiles of a partial round (< CUs / 2)
+// k_edge16_layer only from 256 row tiles (32 per XCD) on: 64x20 (100 row tiles, 12-13 per XCD, mostly
+// inside the layer-2 lag) measured 0.186 vs 0.176 ms for the two launches; 64x40 (400) gains 5%
+constexpr long kLayerMinTiles = 256;
 
 struct chm_model {
   chm_dims d;
@@ -1048,7 +1051,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (e2.rtiles && m->edge_layer && !m->edge_trace) {
+      if (e2.rtiles && m->edge_layer && b->nrt >= kLayerMinTiles && !m->edge_trace) {
         // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
         e1.lflags = e2.lflags = b->lflags;
         e1.xbad = e2.xbad = b->xbad + l;
