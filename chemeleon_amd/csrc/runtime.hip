@@ -731,6 +731,21 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   return CHM_OK;
 }
 
+extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
+  if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
+  BatchTables t;
+  int rc = batch_tables(h_natoms, B, t);
+  if (rc) return rc;
+  std::vector<int4> rt;
+  const long r2 = row_tiles(t, &rt);
+  if (r2tot) *r2tot = r2;
+  if (out4 && cap4 >= 4 * (int64_t)rt.size())
+    for (size_t k = 0; k < rt.size(); ++k) {
+      out4[4 * k] = rt[k].x; out4[4 * k + 1] = rt[k].y; out4[4 * k + 2] = rt[k].z; out4[4 * k + 3] = rt[k].w;
+    }
+  return (int)rt.size();
+}
+
 extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, chm_batch** out) {
   return batch_build(m, h_natoms, B, max_pairs, nullptr, 0, nullptr, out);
 }

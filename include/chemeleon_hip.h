@@ -265,6 +265,13 @@ int chm_debug_d3pm_philox(int N, int A, int T, const float* d_logits, const int6
                           const float* d_q_one_step, const float* d_q_mats, uint64_t seed, int64_t node_base,
                           int64_t* d_out, void* stream);
 
+/* Host-only test hook (no device): the row tiles edge layer 2 runs on for an fc batch of these
+ * crystals (EdgeArgs::rtiles; DESIGN.md "Edge layer 2 on row tiles"). Returns the tile count R (or a
+ * negative CHM_E_*); if out4 holds >= 4 R int32 it receives per tile {first node starting in the tile,
+ * first node starting after it, the node continued from the previous tile or -1, that node's row
+ * offset in the continued-rows buffer}, and *r2tot the buffer's rows. */
+int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot);
+
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */
 int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* stream);
