@@ -151,9 +151,10 @@ def cpu_baseline(n_samples, n_atoms, steps):
 def api_legs(model, n_samples, n_atoms, cond, null, seed, headline):
     """What a drop-in caller gets (reference chemeleon.py:469-490): Chemeleon.sample() end to end
     in perf mode (one captured HIP graph replayed per timestep, device Philox noise), including
-    graph capture, the final device->host copy and get_atoms; and the per-step cost of the
-    parity mode (noise='torch': the reference's CPU RNG stream drawn and uploaded every step,
-    eager launches)."""
+    graph capture, the final device->host copy and get_atoms; the same call in the default
+    parity mode (noise='torch': the reference's CPU RNG stream drawn on the host every step and
+    copied in before each replay of the captured step) over 30 steps; and parity mode's eager
+    per-step cost (graph=False, the round-1 path)."""
     out = {}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -166,20 +167,24 @@ def api_legs(model, n_samples, n_atoms, cond, null, seed, headline):
                                   "ratio_to_headline": (n_samples / dt) / headline,
                                   "call": f"Chemeleon.sample(n_atoms={n_atoms}, n_samples={n_samples}, "
                                           "noise='philox') incl. graph capture and get_atoms"}
-    it = model.sample_states([n_atoms] * n_samples, None, 2.0, 1e-5, noise="torch", text_embeds=cond,
-                             null_text_embeds=null, clone=False)
-    next(it)
-    next(it)  # warm-up step
-    torch.cuda.synchronize()
-    steps = 3
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for key, graph, steps, note in (
+            ("torch_noise_graph_step", True, 30, "noise='torch' (parity mode, the default of sample()): host RNG "
+                                                 "draw into pinned buffers, copy, replay of the captured step"),
+            ("torch_noise_step", False, 3, "noise='torch' with graph=False: host RNG draw + upload per step, eager "
+                                           "launches")):
+        it = model.sample_states([n_atoms] * n_samples, None, 2.0, 1e-5, noise="torch", text_embeds=cond,
+                                 null_text_embeds=null, clone=False, graph=graph)
         next(it)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    it.close()
-    out["torch_noise_step"] = {"ms_per_step": ms, "structures_per_sec": n_samples / (ms * 1e-3 * T_STEPS),
-                               "note": "noise='torch' (parity mode): host RNG draw + upload per step, eager launches"}
+        next(it)  # warm-up step (and graph capture)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            next(it)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        it.close()
+        out[key] = {"ms_per_step": ms, "structures_per_sec": n_samples / (ms * 1e-3 * T_STEPS), "steps": steps,
+                    "note": note}
     return out
 
 

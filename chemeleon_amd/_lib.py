@@ -87,6 +87,9 @@ SIGNATURES = {
                                 c_void_p]),
     "chm_sample_step_dt": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_u64, c_i64, c_i64, c_void_p]),
+    "chm_sample_step_dt_noise": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
     "chm_segment_mean": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "chm_d3pm_sample": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),

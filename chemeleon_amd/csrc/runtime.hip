@@ -1216,6 +1216,16 @@ extern "C" int chm_sample_step_dt(chm_batch* b, const chm_schedule* sc, int32_t*
                      seed, node_base, graph_base, (hipStream_t)stream);
 }
 
+extern "C" int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sc, int32_t* d_t, float cond_scale,
+                                        int64_t* d_a, float* d_x, float* d_l, const float* d_cond, const float* d_null,
+                                        const float* ra, const float* rl, const float* rx1, const float* rx2,
+                                        void* stream) {
+  if (!d_t) return fail(CHM_E_ARG, "d_t is NULL");
+  if (!ra || !rl || !rx1 || !rx2) return fail(CHM_E_ARG, "all four noise buffers are required");
+  return sample_step(b, sc, 0, d_t, cond_scale, d_a, d_x, d_l, d_cond, d_null, ra, rl, rx1, rx2, 0, 0, 0,
+                     (hipStream_t)stream);
+}
+
 extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, float* agg, void* stream) {
   if (!b || !msg || !agg) return fail(CHM_E_ARG, "NULL argument");
   if (pairs < 1) return fail(CHM_E_ARG, "pairs must be >= 1");

@@ -310,9 +310,14 @@ class Chemeleon(nn.Module):
         (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
         starting with the pure-noise state at t = T.
 
-        graph=True (noise="philox" only; the default in that mode): one reverse
-        step is captured once as a HIP graph (chm_sample_step_dt reads t from
-        device memory and decrements it) and replayed for every timestep.
+        graph=True (the default on fc batches): one reverse step is captured once
+        as a HIP graph (chm_sample_step_dt reads t from device memory and
+        decrements it) and replayed for every timestep. With noise="torch" the
+        step reads its noise from fixed device buffers (chm_sample_step_dt_noise):
+        every step's draws come from the CPU generator in the reference's order
+        (rand(N, A), randn(B, 3, 3), randn(N, 3), randn(N, 3)), into pinned host
+        buffers (two, alternating, so the next draw overlaps the running step)
+        and are copied in stream order before the replay.
 
         Initial noise: from `init` = (l_T [B,3,3], x_T [N,3]) if given, else drawn
         on the CPU from the global generator (noise="torch", chemeleon.py:348-349)
@@ -340,7 +345,7 @@ class Chemeleon(nn.Module):
             raise ValueError("noise must be 'torch' or 'philox'")
         knn = getattr(self.decoder, "edge_style", "fc") == "knn"
         if graph is None:  # knn edges are rebuilt from the coordinates with a host sync: eager only
-            graph = noise == "philox" and not knn
+            graph = not knn
         if graph and knn:
             raise ValueError("edge_style='knn' rebuilds its edges every decoder call and cannot run as a captured graph")
         dev = self.device
@@ -369,9 +374,13 @@ class Chemeleon(nn.Module):
         stream = _lib.stream_handle(dev)
         emit = (lambda *ts: tuple(t.clone() for t in ts)) if clone else (lambda *ts: ts)
         yield (T,) + emit(a, x, lat)
+        if graph and noise == "torch":
+            if lanes > 1:
+                raise ValueError("lanes > 1 needs noise='philox'")
+            yield from self._replay_torch_noise(batch, sched, a, x, lat, cond, null, cond_scale, N, B, A, T, t_stop,
+                                                emit)
+            return
         if graph:
-            if noise != "philox":
-                raise ValueError("graph=True needs noise='philox' (host noise cannot be replayed)")
             from ..distributed import partition
             groups = partition(natoms, max(1, min(int(lanes), B)))
             d_t = torch.full((len(groups),), T, dtype=torch.int32, device=dev)
@@ -423,6 +432,43 @@ class Chemeleon(nn.Module):
                                          seed, node_base, graph_base, stream), "chm_sample_step")
             yield (t - 1,) + emit(a, x, lat)
 
+    def _replay_torch_noise(self, batch, sched, a, x, lat, cond, null, cond_scale, N, B, A, T, t_stop, emit):
+        """Parity-mode noise (the reference's CPU RNG stream) under one captured reverse step."""
+        dev = self.device
+        L = _lib.load()
+        d_t = torch.full((1,), T, dtype=torch.int32, device=dev)
+        shapes = ((N, A), (B, 3, 3), (N, 3), (N, 3))
+        dnz = [torch.zeros(sh, dtype=torch.float32, device=dev) for sh in shapes]
+        pin = [[torch.empty(sh, dtype=torch.float32).pin_memory() for sh in shapes] for _ in range(2)]
+        done = [None, None]  # event after the last copy out of each pinned set
+        hg = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(hg, stream=side):
+                _lib.check(L.chm_sample_step_dt_noise(
+                    batch.handle, sched, _lib.ptr(d_t), float(cond_scale), _lib.ptr(a), _lib.ptr(x), _lib.ptr(lat),
+                    _lib.ptr(cond), _lib.ptr(null), *[_lib.ptr(z) for z in dnz], _lib.stream_handle(dev)),
+                    "chm_sample_step_dt_noise")
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_stream(side)
+        d_t.fill_(T)
+        for t in range(T, t_stop, -1):
+            if t > 1:  # chemeleon.py:400-404, 418, 435, 455 (none at t = 1)
+                k = t & 1
+                if done[k] is not None:
+                    done[k].synchronize()  # the copy of two steps ago has left this pinned set
+                torch.rand(shapes[0], out=pin[k][0])
+                torch.randn(shapes[1], out=pin[k][1])
+                torch.randn(shapes[2], out=pin[k][2])
+                torch.randn(shapes[3], out=pin[k][3])
+                for dz, pz in zip(dnz, pin[k]):
+                    dz.copy_(pz, non_blocking=True)
+                done[k] = torch.cuda.Event()
+                done[k].record(cur)
+            hg.replay()
+            yield (t - 1,) + emit(a, x, lat)
+
     @torch.no_grad()
     def reverse_step(self, t: int, atom_types, frac_coords, lattices, natoms: List[int], cond_scale: float = 2.0,
                      step_lr: float = 1e-5, text_embeds=None, null_text_embeds=None, noise=None, seed: int = 0,
@@ -465,9 +511,9 @@ class Chemeleon(nn.Module):
                return_trajectory: bool = False, stream: bool = False, **kw):
         """chemeleon.py:469-490. Without return_trajectory / stream, only the
         final state is copied to the host (the reference converts every step).
-        Keyword arguments go to sample_states: noise="philox" (device noise,
-        one captured HIP graph replayed per timestep) or the default
-        noise="torch" (the reference's CPU RNG stream, eager launches)."""
+        Keyword arguments go to sample_states: noise="philox" (device noise)
+        or the default noise="torch" (the reference's CPU RNG stream); either
+        way one captured HIP graph is replayed per timestep (fc edges)."""
         natoms = [n_atoms] * n_samples
         texts = [text_input] * n_samples if text_input is not None else None
         if stream:

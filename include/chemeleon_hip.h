@@ -240,6 +240,14 @@ int chm_sample_step_dt(chm_batch* b, const chm_schedule* sched, int32_t* d_t, fl
                        float* d_x, float* d_l, const float* d_cond, const float* d_null, uint64_t seed,
                        int64_t node_base, int64_t graph_base, void* stream);
 
+/* The same with the noise read from fixed device buffers (d_rand_* as in chm_sample_step, all four):
+ * the caller refills them before every replay (the reference's CPU RNG stream drawn on the host and
+ * copied in stream order), so parity-mode sampling also runs as one captured step. At t == 1 the
+ * buffers are not read (their stale contents are finite uniforms / normals). */
+int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale, int64_t* d_a,
+                             float* d_x, float* d_l, const float* d_cond, const float* d_null, const float* d_rand_a,
+                             const float* d_rand_l, const float* d_rand_x1, const float* d_rand_x2, void* stream);
+
 /* Standalone message-passing aggregation (scatter_mean of edge messages onto
  * their source node; chemeleon/utils/scatter.py:88-112 as called from
  * cspnet.py:155-160) over this batch's fc edge layout:

@@ -553,6 +553,25 @@ def test_graph_replay_matches_eager(model100, cn, lanes):
             assert torch.equal(se[k], sg[k]), f"t={se[0]} state {k}"
 
 
+def test_torch_noise_graph_matches_eager(model100, cn):
+    """Parity mode (noise='torch', the reference's CPU RNG stream) under the captured step: every
+    step's draws go through pinned host buffers into fixed device buffers before the replay. The
+    whole T = 100 trajectory (down to t = 0, where no noise is drawn) equals eager stepping bit for
+    bit, and the CPU generator ends in the same state."""
+    nat = [5, 9, 3, 12, 7, 1, 20]
+    runs, after = [], []
+    for graph in (False, True):
+        torch.manual_seed(1234)
+        runs.append(list(model100.sample_states(nat, None, 2.0, 1e-5, noise="torch", text_embeds=cn[0],
+                                                null_text_embeds=cn[1], clone=True, graph=graph)))
+        after.append(torch.rand(4))
+    assert [s[0] for s in runs[0]] == [s[0] for s in runs[1]] and runs[0][-1][0] == 0
+    for se, sg in zip(*runs):
+        for k in (1, 2, 3):
+            assert torch.equal(se[k], sg[k]), f"t={se[0]} state {k}"
+    assert torch.equal(after[0], after[1]), "the CPU generator consumed a different number of draws"
+
+
 def test_large_batch_step_is_finite(model1000, cn):
     """512 x 40 (BASELINE metric shape): one reverse step in perf mode."""
     nat = [40] * 512
