@@ -301,6 +301,35 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
             assert torch.equal(u, v), f"{what}: {name} differ from node-aligned segment tiles"
 
 
+def test_one_grid_edge_layers_single_conditioning(cn):
+    """k_edge16_layer with one conditioning (P = 1: a plain decoder call, as the CrystalClip graph
+    encoder and `CSPNet.forward` make): 64 x 40 (400 row tiles, above the one-grid threshold) and a
+    ragged batch, decoder outputs bit-identical to the two-launch schedule, also with the repair
+    launches forced."""
+    model = _model(1000)
+    for nat in ([40] * 64, torch.randint(1, 81, (160,), generator=torch.Generator().manual_seed(5)).tolist()):
+        B, N = len(nat), sum(nat)
+        g = torch.Generator().manual_seed(21)
+        at = torch.randint(0, 100, (N,), generator=g).to(DEV)
+        fr = torch.rand(N, 3, generator=g).to(DEV)
+        la = (torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)).to(DEV)
+        te = model.time_embed(torch.full((B,), 300, dtype=torch.long)).to(DEV)
+        nat_t = torch.tensor(nat)
+        outs = []
+        for layer, repair in ((0, 0), (1, 0), (1, 1)):
+            model.decoder.set_option("edge_layer", layer)
+            model.decoder.set_option("edge_layer_repair", repair)
+            o = model.decoder(atom_types=at, frac_coords=fr, lattices=la, num_atoms=nat_t.to(DEV),
+                              node2graph=torch.arange(B).repeat_interleave(nat_t).to(DEV), t=te,
+                              text_embeds=cn[0].expand(B, -1).to(DEV))
+            outs.append([o.node_features.cpu(), o.atom_types_out.cpu(), o.coords_out.cpu(), o.lattice_out.cpu()])
+        for k in (1, 2):
+            for u, v in zip(outs[0], outs[k]):
+                assert torch.equal(u, v), f"one-grid (repair={k - 1}) differs from two launches, P = 1, B = {B}"
+    del model
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("tag", ["64x20", "16x40"])
 def test_teacher_forced_steps_edge32_kernels(golden, cn, tag):
     """The round-1 split16 edge kernels (v_mfma_f32_32x32x16_f16, k_edge_gemm; option edge16 = 0)
