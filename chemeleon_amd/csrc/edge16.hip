@@ -653,26 +653,30 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile rows and the node list are in LDS
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      const int col = tid & 127;
+      // one wave per node, two adjacent columns per lane (8 node slots: a tile's ~6 nodes of 40 edges run
+      // side by side instead of two per slot); each column is still one sequential sum over its rows
+      const int col = 2 * (tid & 63);
       const int gcol = n0 + half * 128 + col;
-      // the mean of a node over this wave's 64 columns (a wave = one node)
-      auto finish = [&](int node, float sacc, int cnt) __attribute__((always_inline)) {
-        const float mean = sacc / (float)(cnt < 1 ? 1 : cnt);
-        if (!(g.dbg & 4)) g.agg[((long)seg_c * g.nnodes + node) * H + gcol] = mean;
+      auto finish = [&](int node, f32x2e sacc, int cnt) __attribute__((always_inline)) {
+        const float dv = (float)(cnt < 1 ? 1 : cnt);
+        f32x2e mean;
+        mean.x = sacc.x / dv;
+        mean.y = sacc.y / dv;
+        if (!(g.dbg & 4)) *reinterpret_cast<f32x2e*>(g.agg + ((long)seg_c * g.nnodes + node) * H + gcol) = mean;
         if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it
-          float m = fabsf(mean);
+          float m = fmaxf(fabsf(mean.x), fabsf(mean.y));
 #pragma unroll
           for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
           if (lane == 0) atomicMax(g.agg_max + (long)seg_c * g.nnodes + node, __float_as_uint(m));
         }
       };
-      // row tiles: one counter per (conditioning, boundary tile, column group of 64)
-      const int cidx = (n0 / BN) * 4 + half * 2 + (col >> 6);
-      for (int k = tid >> 7; k < nn && !(g.dbg & 32); k += 4) {  // (dbg 32: profiling, no sums)
+      // row tiles: one counter per (conditioning, boundary tile, column half)
+      const int cidx = (n0 / BN) * 4 + half * 2;
+      for (int k = tid >> 6; k < nn && !(g.dbg & 32); k += 8) {  // (dbg 32: profiling, no sums)
         const int2 nk = info[k];
         const int4 ni = {nk.y & 1023, (nk.y >> 10) & 1023, nk.x, nk.y >> 20};  // {rows, first row, node, kind}
         const float* src = T + ni.y * SEG_TP + col;
-        float sacc = 0.f;
+        f32x2e sacc = {0.f, 0.f};
         bool own = true;  // this wave finishes the node
         if (ni.w == 2) {
           // The rest of a node begun in tile t-1, whose head wave publishes the partial sum of its rows
@@ -689,7 +693,10 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           }
           if (__builtin_amdgcn_readfirstlane(v) == 0u) {
             float* mb = g.msgbuf + ((long)seg_c * g.r2tot + g.rtiles[rtile].w) * H + gcol;
-            for (int r = 0; r < ni.x; ++r) st_agent(mb + (long)r * H, src[r * SEG_TP]);
+            for (int r = 0; r < ni.x; ++r) {
+              st_agent(mb + (long)r * H, src[r * SEG_TP]);
+              st_agent(mb + (long)r * H + 1, src[r * SEG_TP + 1]);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (written through before the count)
             unsigned old = 0;
             if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -697,20 +704,22 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           }
           if (own) {
             asm volatile("" ::: "memory");
-            sacc = ld_agent(g.sbuf + ((long)seg_c * g.ntiles + rtile) * H + gcol);
+            const float* sb = g.sbuf + ((long)seg_c * g.ntiles + rtile) * H + gcol;
+            sacc.x = ld_agent(sb);
+            sacc.y = ld_agent(sb + 1);
             if (lane == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (next launch)
           }
         }
         if (own) {
           int jj = 0;
           for (; jj + 8 <= ni.x; jj += 8) {
-            float v[8];
+            f32x2e v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = src[(jj + u) * SEG_TP];
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x2e*>(src + (jj + u) * SEG_TP);
 #pragma unroll
             for (int u = 0; u < 8; ++u) sacc += v[u];
           }
-          for (; jj < ni.x; ++jj) sacc += src[jj * SEG_TP];
+          for (; jj < ni.x; ++jj) sacc += *reinterpret_cast<const f32x2e*>(src + jj * SEG_TP);
         }
         if (ni.w == 0) {
           finish(ni.z, sacc, ni.x);
@@ -721,7 +730,9 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           // has already left its rows in msgbuf, finish the node here
           const long tb = rtile + 1;
           unsigned* cnt = g.rcnt + ((long)seg_c * g.ntiles + tb) * 8 + cidx;
-          st_agent(g.sbuf + ((long)seg_c * g.ntiles + tb) * H + gcol, sacc);
+          float* sb = g.sbuf + ((long)seg_c * g.ntiles + tb) * H + gcol;
+          st_agent(sb, sacc.x);
+          st_agent(sb + 1, sacc.y);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (written through before the count)
           unsigned old = 0;
           if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -731,7 +742,10 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
             const int deg = g.node_n[ni.z];
             const int r2 = deg - ni.x;  // the node's rows in tile t+1
             const float* mb = g.msgbuf + ((long)seg_c * g.r2tot + g.rtiles[tb].w) * H + gcol;
-            for (int r = 0; r < r2; ++r) sacc += ld_agent(mb + (long)r * H);
+            for (int r = 0; r < r2; ++r) {
+              sacc.x += ld_agent(mb + (long)r * H);
+              sacc.y += ld_agent(mb + (long)r * H + 1);
+            }
             finish(ni.z, sacc, deg);
           }
         }
