@@ -90,7 +90,7 @@ struct EdgeArgs {
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
-            // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU,
+            // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU (SEGMEAN),
             // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN); bit 6 (tests, exact
             // results) = row tiles never wait for the previous tile's partial sums (msgbuf path); bit 9
             // (tests, exact results) = k_edge16_layer's layer-2 tiles always request the repair launches

@@ -479,8 +479,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
             const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
-            const f32x2e x = (g.dbg & 8) ? (a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]}  // (profiling)
-                                         : silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]});
+            const f32x2e x = silu_e2((a2 + f32x2e{p[e], p[e + 1]}) + f32x2e{q[e], q[e + 1]});
             mx = fmaxf(mx, fmaxf(fabsf(x.x), fabsf(x.y)));
             v[j][e] = x.x;
             v[j][e + 1] = x.y;
@@ -630,7 +629,10 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
           const f32x2e s2 = f32x2e{scv[j & 1][e], scv[j & 1][e + 1]} * rs[i];
           const f32x2e y = a2 * s2 + f32x2e{bbv[j & 1][e], bbv[j & 1][e + 1]};
-          const f32x2e x = (g.dbg & 8) ? y : silu_e2(y);  // (dbg 8: profiling)
+          // (dbg 8: profiling. Removing this uniform select from the epilogue made edge layer 2 ~3% slower
+          // under the compiler's schedule, profiles/r2/layer/epilogue_select_ab.txt, so it stays; the
+          // layer-1 epilogue's copy was removed: -14% VALU instructions in k_edge16<1>)
+          const f32x2e x = (g.dbg & 8) ? y : silu_e2(y);
           acc[i][j][e] = x.x;
           acc[i][j][e + 1] = x.y;
         }
