@@ -131,6 +131,8 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
 hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s);
 // both edge layers in one grid (row tiles; layer-2 tiles of row tile i - lag behind layer 1's row tile i)
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s);
+long edge16_layer_blocks(long R, int P);                        // its grid size
+void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map
 hipError_t edge16_init();
 hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,

@@ -62,6 +62,33 @@ __device__ __forceinline__ unsigned xcc_id() {
 
 }  // namespace
 
+// k_edge16_layer's block -> job map (host and device: chm_debug_layer_jobs tests it). XCD x = b % 8
+// walks row tiles [R x / 8, R (x + 1) / 8) as groups i = 0 .. n + d - 1: layer-1 tiles (i, 0), (i, 1)
+// while i < n, then the layer-2 tiles of row tile i - d (P conditionings x 2 column tiles) from i = d.
+// kind 0 = no job (padding), 1 = layer 1 with tile index bid = row tile * 2 + column tile, 2 = layer 2
+// with bid = (row tile * P + conditioning) * 2 + column tile.
+struct LayerJob { int kind; long bid; };
+__host__ __device__ inline LayerJob layer_job(long b, long R, int P, int D) {
+  const long x = b & 7, k = b >> 3;
+  const long lo = R * x / 8, hi = R * (x + 1) / 8, n = hi - lo;
+  const long G = 2 + 2L * P, d = D < n ? D : n;
+  long i, s;
+  if (k < 2 * d) {
+    i = k / 2;
+    s = k % 2;
+  } else if (k - 2 * d < (n - d) * G) {
+    i = d + (k - 2 * d) / G;
+    s = (k - 2 * d) % G;
+  } else {
+    const long k2 = k - 2 * d - (n - d) * G;
+    if (k2 >= d * 2 * P) return LayerJob{0, 0};
+    i = n + k2 / (2 * P);
+    s = 2 + k2 % (2 * P);
+  }
+  if (s < 2) return LayerJob{1, (lo + i) * 2 + s};
+  return LayerJob{2, ((lo + i - d) * P + (s - 2) / 2) * 2 + (s - 2) % 2};
+}
+
 // one output tile: virtual block vb of nvb (the XCD-aware remap turns it into a tile index), or the
 // tile index itself (bid_in >= 0). ONE (k_edge16_layer, both edge layers in one grid): layer-2 tiles
 // wait for the layer-1 tiles of their rows (EdgeArgs::lflags) and read S through the XCD's L2, which
@@ -787,29 +814,11 @@ __global__ __launch_bounds__(512, 1) void k_edge16_tail(EdgeArgs g1, EdgeArgs g2
 // storing at once. Dependencies only point to earlier blocks of the same XCD's sequence (dispatched
 // in index order), and the waits are bounded.
 __global__ __launch_bounds__(512, 1) void k_edge16_layer(EdgeArgs g1, EdgeArgs g2, int R, int D) {
-  const int x = blockIdx.x & 7;
-  const long k = blockIdx.x >> 3;
-  const long lo = (long)R * x / 8, hi = (long)R * (x + 1) / 8, n = hi - lo;
-  const int P = g2.npairs, G = 2 + 2 * P;
-  const long d = D < n ? D : n;
-  long i;
-  int s;
-  if (k < 2 * d) {
-    i = k / 2;
-    s = (int)(k % 2);
-  } else if (k - 2 * d < (n - d) * G) {
-    i = d + (k - 2 * d) / G;
-    s = (int)((k - 2 * d) % G);
-  } else {
-    const long k2 = k - 2 * d - (n - d) * G;
-    if (k2 >= d * 2 * P) return;
-    i = n + k2 / (2 * P);
-    s = 2 + (int)(k2 % (2 * P));
-  }
-  if (s < 2)
-    edge16_tile<EPI_EDGE, false, true>(g1, blockIdx.x, gridDim.x, (lo + i) * 2 + s);
-  else
-    edge16_tile<EPI_SEGMEAN, true, true>(g2, blockIdx.x, gridDim.x, ((lo + i - d) * P + (s - 2) / 2) * 2 + (s - 2) % 2);
+  const LayerJob j = layer_job(blockIdx.x, R, g2.npairs, D);
+  if (j.kind == 1)
+    edge16_tile<EPI_EDGE, false, true>(g1, blockIdx.x, gridDim.x, j.bid);
+  else if (j.kind == 2)
+    edge16_tile<EPI_SEGMEAN, true, true>(g2, blockIdx.x, gridDim.x, j.bid);
 }
 
 // Repair of a k_edge16_layer launch whose check failed (*g.xbad != 0: some layer-2 tile read S written
@@ -864,6 +873,18 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t 
   return hipGetLastError();
 }
 
+long edge16_layer_blocks(long R, int P) { return 8 * ((R + 7) / 8) * (2 + 2L * P); }
+
+// (host) the job of every block of a k_edge16_layer grid: out[2 b] = kind, out[2 b + 1] = tile index
+void edge16_layer_jobs(long R, int P, int D, long* out) {
+  const long nb = edge16_layer_blocks(R, P);
+  for (long b = 0; b < nb; ++b) {
+    const LayerJob j = layer_job(b, R, P, D);
+    out[2 * b] = j.kind;
+    out[2 * b + 1] = j.bid;
+  }
+}
+
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s) {
   if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
       !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.row_base != 0 || g1.flags || !g1.lflags ||
@@ -880,8 +901,8 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const long R = g2.ntiles, nmax = (R + 7) / 8;
-  const long blocks = 8 * nmax * (2 + 2L * g2.npairs);
+  const long R = g2.ntiles;
+  const long blocks = edge16_layer_blocks(R, g2.npairs);
   hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

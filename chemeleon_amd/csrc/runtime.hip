@@ -731,6 +731,13 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   return CHM_OK;
 }
 
+extern "C" int64_t chm_debug_layer_jobs(int64_t R, int P, int lag, int64_t* out, int64_t cap) {
+  if (R < 1 || P < 1 || P > 2 || lag < 1) return fail(CHM_E_ARG, "bad arguments");
+  const long nb = edge16_layer_blocks(R, P);
+  if (out && cap >= 2 * nb) edge16_layer_jobs(R, P, lag, reinterpret_cast<long*>(out));
+  return nb;
+}
+
 extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
   if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   BatchTables t;

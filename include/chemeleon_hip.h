@@ -279,6 +279,12 @@ int chm_debug_d3pm_philox(int N, int A, int T, const float* d_logits, const int6
  * first node starting after it, the node continued from the previous tile or -1, that node's row
  * offset in the continued-rows buffer}, and *r2tot the buffer's rows. */
 int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot);
+/* Host-only test hook: the block -> job map of the one-grid edge-layer kernel (k_edge16_layer) for R
+ * row tiles, P conditionings and layer-2 lag `lag`. Returns the grid size nb (or a negative CHM_E_*);
+ * if out holds >= 2 nb int64 it receives per block {kind (0 none, 1 edge layer 1, 2 edge layer 2),
+ * tile index (layer 1: row tile * 2 + column tile; layer 2: (row tile * P + conditioning) * 2 +
+ * column tile)}. */
+int64_t chm_debug_layer_jobs(int64_t R, int P, int lag, int64_t* out, int64_t cap);
 
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */

@@ -70,3 +70,37 @@ def test_row_tiles_reject_bad_batches():
     assert lib.chm_debug_row_tiles(nat, 2, None, 0, None) < 0
     nat = (ctypes.c_int32 * 1)(300)
     assert lib.chm_debug_row_tiles(nat, 1, None, 0, None) < 0
+
+
+@pytest.mark.parametrize("R,P,lag", [(400, 2, 10), (3200, 2, 10), (1367, 1, 10), (256, 2, 1), (300, 2, 3),
+                                     (7, 2, 10), (9, 1, 4), (17500, 2, 10)])
+def test_layer_grid_schedule(R, P, lag):
+    """The one-grid edge-layer kernel's block -> job map (chm_debug_layer_jobs, the same function the
+    kernel runs): every layer-1 tile (row tile, column tile) and every layer-2 tile (row tile,
+    conditioning, column tile) is run by exactly one block, and every layer-2 block comes after both
+    layer-1 blocks of its rows in the same XCD's sequence (blockIdx = XCD + 8 k): the invariant that
+    keeps the in-grid waits free of deadlock (a waiting block's producers were dispatched before it)."""
+    lib = _lib.load()
+    nb = lib.chm_debug_layer_jobs(R, P, lag, None, 0)
+    assert nb > 0
+    out = (ctypes.c_int64 * (2 * nb))()
+    assert lib.chm_debug_layer_jobs(R, P, lag, out, 2 * nb) == nb
+    jobs = np.frombuffer(out, dtype=np.int64).reshape(nb, 2)
+    l1 = {}
+    for b, (kind, bid) in enumerate(jobs):
+        if kind == 1:
+            assert bid not in l1
+            l1[int(bid)] = b
+    assert sorted(l1) == list(range(2 * R))
+    seen = set()
+    for b, (kind, bid) in enumerate(jobs):
+        if kind != 2:
+            continue
+        assert bid not in seen
+        seen.add(int(bid))
+        r = int(bid) // 2 // P
+        for c in (0, 1):
+            p = l1[2 * r + c]
+            assert p < b and p % 8 == b % 8, f"layer-2 block {b} (row tile {r}) before its producer {p}"
+    assert sorted(seen) == list(range(2 * P * R))
+    assert set(jobs[:, 0].tolist()) <= {0, 1, 2}
