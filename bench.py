@@ -30,6 +30,8 @@ One JSON line is printed by rank 0, including:
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -71,7 +73,23 @@ def parse():
     p.add_argument("--ragged", action="store_true",
                    help="SURVEY C4 workload: natoms = randint(1, 81, generator seed 7) per sample (use with "
                         "--n-samples 2048), ranks split by sum of n^2; not the headline metric")
+    p.add_argument("--no-traffic", action="store_true",
+                   help="skip the in-run HBM traffic measurement of the dominant kernel (two rocprofv3 --pmc passes "
+                        "over a 2-step eager probe; roofline.traffic then falls back to the committed profile)")
+    p.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)  # (the PMC passes' workload)
     return p.parse_args()
+
+
+def edge_layer_bytes(natoms, P=2):
+    """Algorithmic HBM bytes of one k_edge16_layer launch (both edge layers of a CSP layer, split16):
+    F read once (E x 768 fp16 hi/lo), S written and read once per conditioning (E x 512 fp16 hi/lo +
+    one packed exponent word per row), the P / Q node halves read, agg written, the split weights
+    D (512 x 768) and W2 (512 x 512) read once."""
+    E = sum(n * n for n in natoms)
+    N = sum(natoms)
+    f = E * FD * 4
+    s = P * E * (H * 4 + 4)
+    return f + 2 * s + P * N * 2 * H * 4 + P * N * H * 4 + (H * FD + H * H) * 4
 
 
 def decoder_pair_flops(natoms, P=2, share_fourier=True):
@@ -188,35 +206,154 @@ def api_legs(model, n_samples, n_atoms, cond, null, seed, headline):
     return out
 
 
-def _pmc_traffic(math, kernel_key):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>/traffic.json;
-    FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE). The counters cannot be
-    read from inside this process, so the value is the one measured on the same command."""
-    if math != "split16":
-        return None, None
+def _stored_traffic(kernel_key):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC profile
+    (tools/pmc_traffic.sh -> tools/traffic_summary.py -> profiles/<round>/traffic.json), with the box
+    that profile ran on: the fallback when the in-run passes are skipped or fail."""
     here = os.path.dirname(os.path.abspath(__file__))
-    for rnd in sorted(os.listdir(os.path.join(here, "profiles")), reverse=True) if os.path.isdir(
-            os.path.join(here, "profiles")) else []:
-        f = os.path.join(here, "profiles", rnd, "traffic.json")
+    pdir = os.path.join(here, "profiles")
+    for rnd in sorted(os.listdir(pdir), reverse=True) if os.path.isdir(pdir) else []:
+        f = os.path.join(pdir, rnd, "traffic.json")
         if os.path.isfile(f):
             try:
-                ks = json.load(open(f))["kernels"]
-                for name, v in ks.items():
+                d = json.load(open(f))
+                for name, v in d["kernels"].items():
                     if kernel_key in name:
-                        return v["bytes_per_launch"], f"profiles/{rnd}/traffic.json ({name})"
+                        return v["bytes_per_launch"], {"source": f"profiles/{rnd}/traffic.json ({name})",
+                                                       "box": d.get("box", "not recorded (an earlier box)")}
             except Exception:  # noqa: BLE001
                 return None, None
     return None, None
 
 
+def _run_pmc_pass(counter, outdir, argv, limit_s):
+    """One `rocprofv3 --pmc <counter>` pass over this script in probe mode, as a child process (the
+    profiler preloads its library into the probe; this process is not re-exec'd), killed with its
+    process group at `limit_s`."""
+    import shutil
+    import signal
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    cmd = [prof, "--pmc", counter, "-d", outdir, "-o", counter.lower(), "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--traffic-probe"] + argv
+    env = dict(os.environ, TMPDIR="/tmp")
+    log = open(os.path.join(outdir + ".log"), "w")
+    p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        rc = p.wait(timeout=limit_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        rc = "timeout"
+    log.close()
+    return rc
+
+
+def measure_traffic(args, kernel_key, limit_s=240):
+    """roofline.traffic measured on this box: FETCH_SIZE and WRITE_SIZE in two rocprofv3 --pmc passes
+    (MI355X_MICROARCH.md: separate passes, FETCH_SIZE x2 on gfx950) over a probe that runs the same
+    workload eagerly for 2 reverse steps; bytes per launch of the dominant kernel."""
+    import tempfile
+    from chemeleon_amd.pmc import box_id, traffic
+    root = tempfile.mkdtemp(prefix="chm_pmc_", dir="/tmp")
+    argv = ["--n-samples", str(args.n_samples), "--n-atoms", str(args.n_atoms), "--math", args.math,
+            "--seed", str(args.seed)]
+    t0 = time.perf_counter()
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        rc = _run_pmc_pass(counter, os.path.join(root, counter.lower()), argv, limit_s)
+        if rc != 0:
+            return None, {"error": f"rocprofv3 --pmc {counter} pass exited with {rc}",
+                          "log": os.path.join(root, counter.lower() + ".log")}
+    ks = traffic(os.path.join(root, "fetch_size"), os.path.join(root, "write_size"))
+    for name, v in ks.items():
+        if kernel_key in name and v["read_bytes"] is not None and v["write_bytes"] is not None:
+            return v["bytes_per_launch"], {
+                "source": f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 2-step eager "
+                          f"probe of the same workload ({name}, {v['launches']} launches)",
+                "read_bytes": v["read_bytes"], "write_bytes": v["write_bytes"],
+                "box": box_id(getattr(torch.cuda.get_device_properties(0), "uuid", None)),
+                "seconds": time.perf_counter() - t0}
+    return None, {"error": f"no {kernel_key} dispatch in the PMC output", "dir": root}
+
+
+def traffic_probe(args):
+    """The PMC passes' workload: this rank's batch, two eager reverse steps (no graph, no timing)."""
+    from chemeleon_amd import Chemeleon
+    from chemeleon_amd.config import default_config
+    from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
+    dev = torch.device("cuda", 0)
+    cfg = default_config()
+    torch.manual_seed(0)
+    model = Chemeleon(cfg)
+    model.decoder.load_state_dict(synthetic_state_dict(cfg))
+    model = model.to(dev).eval()
+    model.decoder.set_math(args.math)
+    cond, null = synthetic_text_embeds(512)
+    it = model.sample_states([args.n_atoms] * args.n_samples, None, 2.0, 1e-5, noise="philox", seed=args.seed,
+                             text_embeds=cond.to(dev), null_text_embeds=null.to(dev), clone=False, t_stop=998,
+                             graph=False)
+    for _ in it:
+        pass
+    torch.cuda.synchronize()
+
+
+def launch_plan(gpus, env, device_count):
+    """What `bench.py --gpus N` does in this process, decided before anything touches the GPU.
+
+    * ("run", None): this process is a rank (WORLD_SIZE set by a launcher, equal to N) or N == 1;
+    * ("spawn", N): N > 1 and no launcher: start N ranks as a child `torch.distributed.run` and
+      forward its output (this process never initialises HIP, so nothing is exec'd from a GPU process);
+    * ("refuse", why): inconsistent requests that would otherwise measure the wrong thing — a
+      launcher's WORLD_SIZE different from --gpus, or more RCCL ranks than visible GPUs (gloo
+      rehearsals, CHM_DIST_BACKEND=gloo, may share one GPU between ranks)."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least one GPU"
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            return "refuse", f"--gpus {gpus} but the launcher's WORLD_SIZE is {world}"
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    backend = env.get("CHM_DIST_BACKEND", "nccl")
+    if backend == "nccl" and device_count < gpus:
+        return "refuse", (f"--gpus {gpus} asks for {gpus} RCCL ranks, one per GPU, but {device_count} GPU(s) are "
+                          "visible (CHM_DIST_BACKEND=gloo rehearses the multi-rank path on fewer GPUs)")
+    return "spawn", gpus
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """Run this script as N ranks under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) and return its exit code; rank 0 prints the JSON line, which passes through."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"bench.py: no launcher found, starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    plan, why = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if plan == "refuse":
+        raise SystemExit(f"bench.py: {why}")
+    if plan == "spawn":
+        raise SystemExit(spawn_ranks(why, sys.argv[1:]))
+    if args.traffic_probe:
+        traffic_probe(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     # One process per GPU. The device is LOCAL_RANK modulo the visible GPUs (the identity on an
     # 8-GPU node); CHM_DIST_BACKEND=gloo rehearses the same path with several ranks sharing one GPU.
     # The two backends differ only in init_process_group.
@@ -272,6 +409,7 @@ def main():
                              null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
                              graph=not args.no_graph, lanes=args.lanes)
     next(it)  # initial state
+    _lib.prof_events(reset=True)  # edge-kernel health counters (wait timeouts, repairs) from here on
     # per-kernel HIP-event instrumentation (eager launches only; graph captures are not instrumented)
     _lib.check(_lib.load().chm_prof_reset(), "prof_reset")
     _lib.check(_lib.load().chm_prof_enable(1), "prof_enable")
@@ -314,10 +452,18 @@ def main():
         torch.cuda.synchronize()
         model.decoder.set_option("edge_layer", 1)
     _lib.check(_lib.load().chm_prof_enable(0), "prof_disable")
+    torch.cuda.synchronize()
+    events = _lib.prof_events()
+    per_rank = [elapsed]
     if dist is not None:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        every = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(every, tt)
+        per_rank = [float(v.item()) for v in every]
+        elapsed = max(per_rank)
+        ev = torch.tensor([events[k] for k in _lib.EVENT_NAMES], device=dev, dtype=torch.float64)
+        dist.all_reduce(ev)  # (summed over ranks)
+        events = {k: int(v) for k, v in zip(_lib.EVENT_NAMES, ev.tolist())}
         # finished structures -> every rank (the all-gather of the sampler; outside the timed region)
         from chemeleon_amd.distributed import gather_states
         gather_states(state[1:], natoms, natoms_all=[all_nat[a:b] for a, b in ranges])
@@ -339,8 +485,18 @@ def main():
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
     edge16 = os.environ.get("CHM_EDGE16", "1") != "0"
     msg_kernel = "k_edge16_layer" if nlay else ("k_edge16<2" if edge16 else "k_edge_gemm<2")
-    traffic, traffic_src = (_pmc_traffic(math, msg_kernel) if not args.ragged else
-                            (None, "not collected for the ragged workload"))
+    traffic, traffic_src = None, "not collected for the ragged workload" if args.ragged else "not collected"
+    if math == "split16" and not args.ragged:
+        if rank == 0 and world == 1 and not args.no_traffic:
+            try:
+                traffic, traffic_src = measure_traffic(args, msg_kernel)
+            except Exception as e:  # noqa: BLE001
+                traffic, traffic_src = None, {"error": repr(e)}
+        if traffic is None and (args.n_samples, args.n_atoms, world) == (512, 40, 1):  # (the stored profile's shape)
+            failed = traffic_src
+            traffic, traffic_src = _stored_traffic(msg_kernel)
+            if traffic_src is not None:
+                traffic_src["in_run"] = failed if not args.no_traffic and world == 1 else "skipped"
     lay_flops = fou_flops + msg_flops
     lay_tflops = lay_flops / (ms_lay / nlay * 1e-3) / 1e12 if nlay else None
     # fp32-equivalent ceilings: bf16x3 = 2.5 PF / 6 products; split16 edge GEMMs = 2.5 PF (fp16 dense
@@ -379,6 +535,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": s_per_step * 1e3,
+        "per_rank_ms_per_step": {"min": min(per_rank) / args.steps * 1e3, "max": max(per_rank) / args.steps * 1e3},
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -408,6 +565,7 @@ def main():
                      "frac": ((lay_tflops if nlay else msg_tflops) / peak) if (lay_tflops or msg_tflops) else None,
                      "traffic": traffic,
                      "traffic_source": traffic_src,
+                     "traffic_algorithmic": (edge_layer_bytes(natoms) if nlay else None),
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
                                    "split16": "fp32-equivalent flops (3 fp16 MFMA products each); fp16 dense MFMA "
                                            "2.5 PF / 3 products",
@@ -434,6 +592,9 @@ def main():
                  "math": math, "flops_per_step_per_gpu": step_flops,
                  "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,
                  "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
+        "edge_repairs": events["layer_repairs"] + events["tail_repairs"],
+        "edge_events": dict(events, note="device counters over warm-up, timed and eager passes (chm_prof_events): "
+                                         "repairs recompute a layer whose intra-grid check failed; 0 = none ran"),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_api_legs and not args.ragged:

@@ -99,6 +99,8 @@ SIGNATURES = {
     "chm_prof_enable": (c_int, [c_int]),
     "chm_prof_reset": (c_int, []),
     "chm_prof_read": (c_int, [c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
+    "chm_prof_events": (c_int, [ctypes.POINTER(c_i64), c_int]),
+    "chm_prof_events_reset": (c_int, []),
 }
 
 
@@ -159,3 +161,17 @@ def prof_read(kernel: int):
     ms = ctypes.c_double()
     check(load().chm_prof_read(kernel, ctypes.byref(n), ctypes.byref(ms)), "chm_prof_read")
     return int(n.value), float(ms.value)
+
+
+EVENT_NAMES = ("layer_wait_timeouts", "layer_other_xcd", "layer_repairs", "tail_wait_timeouts", "tail_repairs")
+
+
+def prof_events(reset: bool = False):
+    """The edge kernels' device health counters (include/chemeleon_hip.h, CHM_EV_*): wait timeouts,
+    cross-XCD reads and the repair launches that ran since the last reset. Synchronous."""
+    v = (c_i64 * 8)()
+    check(load().chm_prof_events(v, 8), "chm_prof_events")
+    out = {name: int(v[k]) for k, name in enumerate(EVENT_NAMES)}
+    if reset:
+        check(load().chm_prof_events_reset(), "chm_prof_events_reset")
+    return out

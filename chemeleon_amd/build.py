@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libchemeleon_hip.so")
-SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "edge_gemm.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip"]
+SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "split16.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip"]
 ARCH = os.environ.get("CHM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -36,15 +36,20 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and not needs_build():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
-    objs = []
-    for src in SOURCES:
+    from concurrent.futures import ThreadPoolExecutor
+
+    def compile_one(src):
         obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src),
                "-o", obj, "-Wno-unused-result"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
-        objs.append(obj)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "4"))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

@@ -45,11 +45,11 @@ struct GemmArgs {
 
 enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 
-// split16 edge GEMMs (edge_gemm.hip): both operands split into fp16 hi/lo, stored per row as
+// split16 edge GEMMs (edge16.hip): both operands split into fp16 hi/lo, stored per row as
 // [K/32][hi 32 | lo 32] (a 32-deep K-tile of a row = one 128-B line), three fp16 MFMA products,
 // staged by global_load_lds.
 struct EdgeArgs {
-  long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M) (k_edge16; k_edge_gemm: row_base 0)
+  long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M)
   long row_base;
   int N, K;
   const void* A;                  // split rows [rows][K/32][2][32] fp16, readable 256 rows past the last
@@ -61,7 +61,7 @@ struct EdgeArgs {
   const int* ei; const int* ej; const float* PQ; long nnodes; int npairs; long E;
   const int* node_off;           // EPI_EDGE: first node of each graph (with natoms, n2g)
   void* S; int* sexp;            // S as split rows [P*E][H/32][2][32] (columns permuted within each
-                                 // 32-chunk, see edge_gemm.hip) + packed chunk exponents
+                                 // 32-chunk, see edge16.hip) + packed chunk exponents
   // EPI_SEGMEAN: agg[c][node] = mean over the node's edges of SiLU(acc + bias)
   const float* bias;
   const int2* tiles; int ntiles;
@@ -81,7 +81,9 @@ struct EdgeArgs {
   // k_edge16_layer (both edge layers in one grid): per row tile, the count of layer-1 column tiles that
   // have written S through, then of the layer-2 tiles that have read it (the last one resets it to 0)
   unsigned* lflags;
-  unsigned* xbad;  // k_edge16_layer: raised by a layer-2 tile that read S of another XCD (repair needed)
+  unsigned* xbad;  // k_edge16_layer: raised by a layer-2 tile that read S of another XCD or whose wait timed
+                   // out; k_edge16_tail: raised by a segment tile whose wait for this grid's layer-1 tiles
+                   // timed out. Either way the repair launches behind the grid recompute the layer.
   // k_edge16_tail: per layer-1 row tile from flag_row0 on, the count of its finished column tiles
   // (EPI_EDGE bumps, EPI_SEGMEAN tiles reading rows >= flag_row0 wait); null = no intra-grid waits.
   // zero_flags / nzero: an EPI_EDGE launch's block 0 clears them for the next grid.
@@ -93,8 +95,18 @@ struct EdgeArgs {
             // barriers, bit 2 = no epilogue stores (EDGE / SEGMEAN); k_edge16 also: bit 3 = no SiLU (SEGMEAN),
             // bit 4 = main loop only (no epilogue), bit 5 = no segment sums (SEGMEAN); bit 6 (tests, exact
             // results) = row tiles never wait for the previous tile's partial sums (msgbuf path); bit 9
-            // (tests, exact results) = k_edge16_layer's layer-2 tiles always request the repair launches
+            // (tests, exact results) = k_edge16_layer's layer-2 tiles always request the repair launches;
+            // bit 13 (tests, exact results) = k_edge16_tail's layer-1 tiles start ~10 ms late and its
+            // segment tiles wait ~2^10 spins only (a real timeout: they read S before it is written);
+            // bit 14 (tests, WRONG results) = no repair launches behind k_edge16_tail
 };
+// Device event counters of the edge kernels (edge16.hip), cumulative over launches and graph replays
+// until chm_prof_events_reset: wait timeouts and repair launches that ran (each must read 0 in a
+// healthy run; a repair doubles the cost of its layer).
+enum { EV_LAYER_TIMEOUT = 0, EV_LAYER_XCD = 1, EV_LAYER_REPAIR = 2, EV_TAIL_TIMEOUT = 3, EV_TAIL_REPAIR = 4,
+       EV_COUNT = 8 };
+hipError_t edge_events_read(unsigned long long* out);  // EV_COUNT values
+hipError_t edge_events_reset();
 // knn (radius-graph) edges, knn.hip: per-crystal scratch at cand_off[b] (n^2 * 27 entries; the final
 // list at 2 * cand_off[b]), outputs sorted by source node into ei / ej / fd at node_estart
 struct KnnArgs {
@@ -122,19 +134,18 @@ struct TrainArgs {
 };
 hipError_t train_noise(const TrainArgs& g, hipStream_t s);
 hipError_t train_loss(const TrainArgs& g, hipStream_t s);
-hipError_t edge_gemm(const EdgeArgs& g, int epi, hipStream_t s);
-hipError_t edge_gemm_init();
-// the same kernels on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)
+// the split16 edge GEMMs on v_mfma_f32_16x16x32_f16 (edge16.hip; S / W2 column permutation 2)
 hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
 // one grid: edge layer 1 (EPI_EDGE, g1: a row range) first, then edge layer 2 (EPI_SEGMEAN, g2: segment
 // tiles that read none of g1's rows)
-hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s);
+// g2.xbad: raised on a timed-out wait; the repair launches behind the grid then recompute layer 2
+hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_grid, hipStream_t s);
 // both edge layers in one grid (row tiles; layer-2 tiles of row tile i - lag behind layer 1's row tile i)
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s);
 long edge16_layer_blocks(long R, int P);                        // its grid size
 void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map
 hipError_t edge16_init();
-hipError_t edge_gemm_variant(const EdgeArgs& g, int var, hipStream_t s);  // (-DCHM_MICROBENCH builds only)
+// (split16.hip) W -> row-scaled split rows (perm 0, or 2 = k_edge16's S column order for W2)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);
 hipError_t fourier_h(const float* x, const int* ei, const int* ej, long E, void* F, hipStream_t s,

@@ -1,13 +1,13 @@
 // The two split16 edge GEMMs of a CSP layer (cspnet.py:134-160: edge_mlp over all n^2 edges, then
 // scatter_mean) on v_mfma_f32_16x16x32_f16.
 //
-// Same operands, LDS rings, tiles and epilogue contracts as k_edge_gemm (edge_gemm.hip): split
-// rows [K/32][hi 32 | lo 32] fp16 staged by global_load_lds into a 3-deep A ring and a 2-deep W
-// ring, 256x256 output tiles, 8 waves of 64 rows x 128 columns, one block per CU, three fp16 MFMA
-// products per fp32 product. What differs is the MFMA shape. Both shapes run the matrix pipe at the
-// same FLOP per cycle, but under load the chip holds a higher clock on 16x16x32: back-to-back on
-// random operands at two waves per SIMD, 1.91 GHz against 1.67 GHz for 32x32x16 (+14% FLOP/s,
-// tools/mfma_shape_probe.hip, profiles/r2/mfma_shape_probe.log).
+// Split rows [K/32][hi 32 | lo 32] fp16 (split16.hip) staged by global_load_lds into a 3-deep A ring
+// and a 2-deep W ring, 256x256 output tiles, 8 waves of 64 rows x 128 columns, one block per CU,
+// three fp16 MFMA products per fp32 product. The MFMA shape: both 16x16x32 and 32x32x16 run the matrix
+// pipe at the same FLOP per cycle, but under load the chip holds a higher clock on 16x16x32: back-to-
+// back on random operands at two waves per SIMD, 1.91 GHz against 1.67 GHz for 32x32x16 (+14% FLOP/s,
+// tools/mfma_shape_probe.hip, profiles/r2/mfma_shape_probe.log; the round-1 32x32x16 kernels were
+// removed in round 3).
 //
 // Per K-tile of 32 a wave reads its four 16-row A fragments and, in four quarters of 32 columns,
 // its W fragments (lane l: row l & 15, k-chunk l >> 4 of the 128-B line, XOR-swizzled so every
@@ -52,6 +52,11 @@ __device__ __forceinline__ void st_agent(float* p, float v) {
 }
 __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// edge_events_* (chm_internal.h): wait timeouts and repairs, counted on the device
+__device__ unsigned long long g_edge_events[EV_COUNT];
+__device__ __forceinline__ void count_event(int k) {
+  __hip_atomic_fetch_add(&g_edge_events[k], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // the XCD (XCC) this wave runs on
 __device__ __forceinline__ unsigned xcc_id() {
@@ -140,7 +145,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     }
   };
 
-  // ---- glds sources (as k_edge_gemm): wave w stages rows 32w..32w+31 of both operands, 8 rows per
+  // ---- glds sources: wave w stages rows 32w..32w+31 of both operands, 8 rows per
   // instruction; lane -> row 32w + 8q + (lane >> 3), LDS chunk lane & 7 holding line chunk
   // (lane & 7) ^ swz(row), swz(row) = (row >> 1) & 7. A rows past nrows are read unclamped (F and S
   // carry 256 rows of padding; those rows' results are never stored).
@@ -173,21 +178,33 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   };
 
   if (EPI == EPI_EDGE && g.zero_flags && vb == 0 && tid < g.nzero) g.zero_flags[tid] = 0u;  // (for the next grid)
+  if (EPI == EPI_EDGE && g.flags && (g.dbg & 8192))  // (tests: the segment tiles' waits time out)
+    for (int k = 0; k < 2500; ++k) __builtin_amdgcn_s_sleep(127);
   if (EPI == EPI_SEGMEAN && g.flags) {
     // k_edge16_tail: a segment tile whose edge rows reach into [flag_row0, E) waits until the layer-1
     // tiles of this grid that write those rows (dispatched first, never waiting themselves) have
     // published them, then acquires at agent scope before any load of S or its exponents. The spin
     // is bounded (~0.3 s), so a broken invariant can never hang the device.
+    // A wait that times out raises *g.xbad (and counts EV_TAIL_TIMEOUT): this tile then goes on with S
+    // that may not be written, and the repair launches behind the grid recompute edge layer 2.
     const long e0 = row0 - (long)seg_c * g.E, e1 = e0 + nrows;
     if (e1 > g.flag_row0) {
       if (tid == 0) {
         const long lo = (e0 > g.flag_row0 ? e0 : g.flag_row0) - g.flag_row0, hi = e1 - 1 - g.flag_row0;
         const unsigned need = (unsigned)(g.N / BN);
+        const unsigned limit = (g.dbg & 8192) ? (1u << 10) : (1u << 21);
+        bool late = false;
         for (long r = lo / BM; r <= hi / BM; ++r) {
           unsigned spins = 0;
-          while (__hip_atomic_load(g.flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&
-                 ++spins < (1u << 21))
+          while (__hip_atomic_load(g.flags + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need && spins < limit) {
+            ++spins;
             __builtin_amdgcn_s_sleep(4);
+          }
+          late |= spins >= limit;
+        }
+        if (late && g.xbad) {
+          __hip_atomic_store(g.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          count_event(EV_TAIL_TIMEOUT);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
@@ -207,8 +224,11 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
              ++spins < (1u << 21))
         __builtin_amdgcn_s_sleep(4);
       const unsigned me = xcc_id() + 1u;
-      if (((v >> 8) & 15u) != me || ((v >> 12) & 15u) != me || (v & 0xffu) < need || (g.dbg & 512))
+      const bool timeout = (v & 0xffu) < need, other = ((v >> 8) & 15u) != me || ((v >> 12) & 15u) != me;
+      if (timeout || other || (g.dbg & 512))
         __hip_atomic_store(g.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (timeout) count_event(EV_LAYER_TIMEOUT);
+      else if (other) count_event(EV_LAYER_XCD);
       const unsigned last = need + 2u * (unsigned)g.npairs - 1u;
       if ((__hip_atomic_fetch_add(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xffu) == last)
         __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -296,7 +316,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     __builtin_amdgcn_sched_group_barrier(0x008, 24 - 2 * nr, 0);
   };
 
-  // prologue (issue order W0 A0 A1 W1 A2, as k_edge_gemm): tile 0 landed when 12 glds remain
+  // prologue (issue order W0 A0 A1 W1 A2): tile 0 landed when 12 glds remain
   issueW(0);
   issueA(0);
   issueA(1);
@@ -312,7 +332,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   // under those MFMAs) when the ring layout allows it (nk % 6 == 0: tiles nk-3, nk-2 sit in A stages
   // 0, 1 and tile nk-1 in A stage 2 / W stage 1) and the rows fit (nR <= PRE_MAX): conditioning 0 at
   // row 0 (A stages 0-1, free after the barrier of tile nk-2), conditioning 1 at row PRE_ROW1 (free
-  // after the barrier of tile nk-1). Same scheme as k_edge_gemm.
+  // after the barrier of tile nk-1).
   bool pre = false;
   int p_ilo = 0, p_jlo = 0, p_nP = 0, p_nR = 0;
   if constexpr (EPI == EPI_EDGE) {
@@ -434,8 +454,8 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   }
 
   if constexpr (EPI == EPI_EDGE) {
-    // S[c][e] = SiLU(D f + P_c[i] + Q_c[j]) as scaled hi/lo fp16 split rows (see k_edge_gemm's
-    // epilogue for the staging of the P / Q rows). First undo the W row scales.
+    // S[c][e] = SiLU(D f + P_c[i] + Q_c[j]) as scaled hi/lo fp16 split rows (the P / Q rows of the
+    // tile's <= 8 source atoms and 1-2 crystals staged in LDS). First undo the W row scales.
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
@@ -604,7 +624,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   if constexpr (EPI == EPI_SEGMEAN) {
     // agg[c][node] = mean over the node's edges of SiLU(acc * wscale * rowscale + b2): the wn-th half
     // of the waves writes its 128 columns to an LDS tile [256][132], then every thread sums node
-    // segments of one column in edge order (scatter_add's order) — as k_edge_gemm.
+    // segments of one column in edge order (scatter_add's order).
     float* T = reinterpret_cast<float*>(lds);
     // node list: {node, rows in this tile | first row in the tile << 10 | kind << 20}; kind 0 = a whole
     // node, 1 = the head part of a node cut at the tile end (row tiles: listed first), 2 = the rest of a
@@ -825,10 +845,12 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer(EdgeArgs g1, EdgeArgs g
 // on another XCD, so its L2 view may have been stale): one layer on the two-launch schedule, grid-
 // stride over the tiles so that the normal case (nothing to repair) costs one small grid that exits.
 // The layer-1 pass also clears the layer's agg row maxima (the failed launch may have max-ed garbage).
+// ev >= 0: count the repair (block 0) as that event.
 template <int EPI, bool ASC>
 __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, unsigned* agg_max, long nmax,
-                                                          unsigned* lflags, long nrt) {
+                                                          unsigned* lflags, long nrt, int ev) {
   if (__hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  if (ev >= 0 && blockIdx.x == 0 && threadIdx.x == 0) count_event(ev);
   if (EPI == EPI_EDGE && agg_max) {  // (and the row-tile flags, in case a wait timed out)
     for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
     for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrt; k += (long)gridDim.x * 512) lflags[k] = 0u;
@@ -851,10 +873,21 @@ hipError_t edge16_init() {
   return hipSuccess;
 }
 
-hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t s) {
+hipError_t edge_events_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_edge_events), sizeof(unsigned long long) * EV_COUNT, 0,
+                             hipMemcpyDeviceToHost);
+}
+
+hipError_t edge_events_reset() {
+  static const unsigned long long zero[EV_COUNT] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_edge_events), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+
+hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_grid, hipStream_t s) {
   if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
       !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.M <= g1.row_base || g1.row_base < 0 ||
-      !g1.flags || g1.flags != g2.flags || g1.flag_row0 != g1.row_base || g2.flag_row0 != g1.row_base)
+      !g1.flags || g1.flags != g2.flags || g1.flag_row0 != g1.row_base || g2.flag_row0 != g1.row_base ||
+      !g2.xbad)
     return hipErrorInvalidValue;
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.tiles || g2.ntiles < 1 || !g2.agg || !g2.bias ||
       !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale ||
@@ -870,6 +903,19 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, hipStream_t 
   const long nb1 = (nt1 + 7) / 8 * 8;
   const long nt2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
   hipLaunchKernelGGL(k_edge16_tail, dim3((unsigned)(nb1 + nt2)), dim3(512), LDS_B, s, g1, g2, (int)nb1, (int)nt1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || (g2.dbg & 16384)) return e;
+  // the repair pair (exits at once unless a segment tile's wait timed out): the first clears layer 2's
+  // agg row maxima (the failed tiles may have max-ed garbage; S itself was complete when the grid
+  // ended), the second recomputes every segment tile of edge layer 2 without intra-grid waits
+  EdgeArgs r1 = g1, r2 = g2;
+  r1.flags = r2.flags = nullptr;
+  r1.xbad = g2.xbad;
+  const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
+  hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, 0L, g2.agg_max,
+                     g2.agg_max ? (long)g2.npairs * g2.nnodes : 0L, (unsigned*)nullptr, 0L, -1);
+  hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nt2, (unsigned*)nullptr,
+                     0L, (unsigned*)nullptr, 0L, (int)EV_TAIL_REPAIR);
   return hipGetLastError();
 }
 
@@ -912,9 +958,9 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
   const long nb1 = ((g1.M + BM - 1) / BM) * (g1.N / BN), nb2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
   const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
   hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, nb1, g2.agg_max,
-                     (long)g2.npairs * g2.nnodes, g1.lflags, R);
+                     (long)g2.npairs * g2.nnodes, g1.lflags, R, -1);
   hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nb2, (unsigned*)nullptr, 0L,
-                     (unsigned*)nullptr, 0L);
+                     (unsigned*)nullptr, 0L, (int)EV_LAYER_REPAIR);
   return hipGetLastError();
 }
 

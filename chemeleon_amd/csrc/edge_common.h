@@ -1,5 +1,5 @@
-// Shared definitions of the split16 edge-GEMM kernels (edge_gemm.hip: 32x32x16 MFMA,
-// edge16.hip: 16x16x32 MFMA). Included inside namespace chm.
+// Shared definitions of the split16 kernels (edge16.hip: the edge GEMMs on 16x16x32 MFMA, split16.hip:
+// operand preparation). Included inside namespace chm.
 #pragma once
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

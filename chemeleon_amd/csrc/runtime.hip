@@ -37,7 +37,7 @@ static int fail(int code, const std::string& msg) {
 struct LayerW {
   const float *WAB, *Wcl, *b1, *D, *W2, *b2, *W3, *b3, *W4, *b4, *lw, *lb;
   const void *WAB3, *D3, *W23, *W33, *W43;  // bf16 hi/mid/lo planes of the GEMM weights
-  void *D2h, *W22h;                          // fp16 hi/lo planes of the edge-GEMM weights (row-scaled)
+  void* D2h;                                 // fp16 hi/lo split rows of the edge-GEMM weights (row-scaled)
   void* W22h16;                              // W2's split rows with k_edge16's K permutation (perm 2)
   float *Dsc, *W2sc;                         // their per-row power-of-two scales
   void *WAB16, *W316, *W416;                 // split16 node GEMMs: fp16 hi/lo rows, 16-column chunks
@@ -66,8 +66,7 @@ struct chm_model {
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
-  int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge_gemm.hip)
-  int edge16 = 1;        // CHM_EDGE16=0: split16 edge GEMMs on the 32x32x16 kernels (k_edge_gemm)
+  int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge16.hip)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
@@ -159,7 +158,6 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
   const int PL = film ? 7 : 1;  // first layer parameter
   {
     hipError_t e0 = gemm_init();
-    if (e0 == hipSuccess) e0 = edge_gemm_init();
     if (e0 == hipSuccess) e0 = edge16_init();
     if (e0 == hipSuccess) e0 = node_gemm_init();
     if (e0 != hipSuccess) return fail(CHM_E_HIP, std::string("gemm_init: ") + hipGetErrorString(e0));
@@ -276,8 +274,6 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
     if (tl) m->edge_trace_layer = atoi(tl);
-    const char* e16 = getenv("CHM_EDGE16");
-    if (e16) m->edge16 = atoi(e16);
     const char* stg = getenv("CHM_EDGE_STAGGER");
     if (stg) m->edge_stagger = atoi(stg);
     const char* spl = getenv("CHM_EDGE_SPLIT");
@@ -323,18 +319,16 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
       p3 += (3 * j.n * 2 + 255) / 256 * 256;
     }
     // fp16 hi/lo planes (+ row scales) of the two edge-GEMM weights of every layer
-    const size_t per_layer = (2 * (size_t)H * FD * 2 + 2 * 2 * (size_t)H * H * 2 + 2 * H * 4 + 1023) / 1024 * 1024;
+    const size_t per_layer = (2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2 + 2 * H * 4 + 1023) / 1024 * 1024;
     e2 = hipMalloc(&m->mem2, per_layer * L);
     for (int l = 0; l < L && e2 == hipSuccess; ++l) {
       char* q = (char*)m->mem2 + per_layer * l;
       LayerW& w = m->layers[l];
       w.D2h = q;
-      w.W22h = q + 2 * (size_t)H * FD * 2;
-      w.W22h16 = q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2;
-      w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * 2 * (size_t)H * H * 2);
+      w.W22h16 = q + 2 * (size_t)H * FD * 2;
+      w.Dsc = (float*)(q + 2 * (size_t)H * FD * 2 + 2 * (size_t)H * H * 2);
       w.W2sc = w.Dsc + H;
       e2 = split_rows_h(w.D, H, FD, w.D2h, w.Dsc, 0, s);
-      if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h, w.W2sc, 1, s);  // K permuted like S
       if (e2 == hipSuccess) e2 = split_rows_h(w.W2, H, H, w.W22h16, w.W2sc, 2, s);  // (k_edge16's S layout)
     }
     // fp16 hi/lo rows (16-column chunks, + row scales) of the node-GEMM weights (split16 node GEMMs)
@@ -390,8 +384,8 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_split = value != 0;
     return CHM_OK;
   }
-  if (k == "edge16") {  // (batches created afterwards; knn batches need the k_edge16 kernels)
-    m->edge16 = value != 0;
+  if (k == "edge16") {  // (the round-1 32x32x16 edge kernels were removed in round 3)
+    if (value == 0) return fail(CHM_E_UNSUPPORTED, "edge16 = 0: the 32x32x16 edge kernels were removed");
     return CHM_OK;
   }
   if (k == "edge_rows") {  // edge layer 2 on 256-row tiles (fc batches) or node-aligned tiles; bit-identical
@@ -409,6 +403,14 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
   }
   if (k == "edge_layer_repair") {  // (tests) k_edge16_layer always runs its repair launches
     m->edge_dbg = value ? (m->edge_dbg | 512) : (m->edge_dbg & ~512);
+    return CHM_OK;
+  }
+  if (k == "edge_tail_timeout") {  // (tests) k_edge16_tail's waits time out (producers delayed), repaired
+    m->edge_dbg = value ? (m->edge_dbg | 8192) : (m->edge_dbg & ~8192);
+    return CHM_OK;
+  }
+  if (k == "edge_tail_norepair") {  // (tests; WRONG results after a timeout) no repair launches behind the tail
+    m->edge_dbg = value ? (m->edge_dbg | 16384) : (m->edge_dbg & ~16384);
     return CHM_OK;
   }
   if (k == "edge_rows_nowait") {  // (tests) row tiles never wait for the previous tile: the msgbuf path
@@ -648,8 +650,8 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   *out = nullptr;
   if (!m || !h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   if (max_pairs < 1 || max_pairs > 2) return fail(CHM_E_ARG, "max_pairs must be 1 or 2");
-  if (bo.knn && (m->math != MATH_SPLIT16 || !m->edge16))
-    return fail(CHM_E_UNSUPPORTED, "knn edges need the split16 arithmetic on the k_edge16 kernels");
+  if (bo.knn && m->math != MATH_SPLIT16)
+    return fail(CHM_E_UNSUPPORTED, "knn edges need the split16 arithmetic (the k_edge16 kernels)");
   BatchTables t;
   int rc = batch_tables(h_natoms, B, t, bo);
   if (rc) return rc;
@@ -876,6 +878,21 @@ extern "C" int chm_prof_read(int kernel, int64_t* launches, double* total_ms) {
   return CHM_OK;
 }
 
+extern "C" int chm_prof_events(int64_t* out, int n) {
+  if (!out || n < 1) return fail(CHM_E_ARG, "NULL argument");
+  unsigned long long v[EV_COUNT];
+  hipError_t e = edge_events_read(v);
+  if (e != hipSuccess) return fail(CHM_E_HIP, std::string("edge_events_read: ") + hipGetErrorString(e));
+  for (int k = 0; k < n; ++k) out[k] = k < EV_COUNT ? (int64_t)v[k] : 0;
+  return CHM_OK;
+}
+
+extern "C" int chm_prof_events_reset(void) {
+  hipError_t e = edge_events_reset();
+  if (e != hipSuccess) return fail(CHM_E_HIP, std::string("edge_events_reset: ") + hipGetErrorString(e));
+  return CHM_OK;
+}
+
 static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const float* W, float* C, long ldc) {
   GemmArgs g;
   std::memset(&g, 0, sizeof(g));
@@ -1021,11 +1038,12 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     }
     HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
   }
-  if (b->xbad && m->edge16 && m->edge_rows && m->edge_layer && b->math == MATH_SPLIT16) {
-    // k_edge16_layer: repair requests and row-tile flags start clear in every call (the flags also
-    // return to 0 at the end of every launch; this keeps a timed-out wait from leaking into later calls)
+  if (b->xbad && b->math == MATH_SPLIT16) {
+    // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[32 + l])
+    // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
+    // launch; this keeps a timed-out wait from leaking into later calls)
     HIPCHK(hipMemsetAsync(b->xbad, 0, 64 * sizeof(unsigned), s));
-    HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
+    if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
@@ -1046,7 +1064,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     if (b->math == MATH_SPLIT16 && E == 0) {  // (knn: no atom within any other's radius: every mean is 0)
       HIPCHK(hipMemsetAsync(b->agg, 0, (size_t)P * N * H * sizeof(float), s));
     } else if (b->math == MATH_SPLIT16) {
-      // split16: fp16 hi/lo split rows throughout (edge_gemm.hip). S lives in S's bytes as
+      // split16: fp16 hi/lo split rows throughout (edge16.hip). S lives in S's bytes as
       // split rows [P*E][H/32][2][32] plus one packed exponent word per row (rowmax buffer).
       int* sexp = reinterpret_cast<int*>(b->rowmax);
       // edge layer 1: S_c = SiLU(D f_ij + P_c[i] + Q_c[j]), D f shared by the pair
@@ -1060,12 +1078,12 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       EdgeArgs e2;
       std::memset(&e2, 0, sizeof(e2));
       e2.M = (long)P * E; e2.N = H; e2.K = H; e2.A = b->S; e2.aexp = sexp;
-      e2.W = m->edge16 ? w.W22h16 : w.W22h; e2.wscale = w.W2sc; e2.bias = w.b2; e2.tiles = b->tiles;
+      e2.W = w.W22h16; e2.wscale = w.W2sc; e2.bias = w.b2; e2.tiles = b->tiles;
       e2.ntiles = b->ntiles;
       e2.node_estart = b->node_estart; e2.natoms = b->natoms; e2.n2g = b->n2g; e2.agg = b->agg;
       e2.node_n = b->node_n; e2.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
       e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
-      if (m->edge16 && m->edge_rows && b->rtiles) {  // 256-row tiles, cut nodes continued across tiles
+      if (m->edge_rows && b->rtiles) {  // 256-row tiles, cut nodes continued across tiles
         e2.rtiles = b->rtiles; e2.ntiles = (int)b->nrt; e2.sbuf = b->sbuf; e2.msgbuf = b->msgbuf;
         e2.rcnt = b->rcnt; e2.r2tot = b->r2tot;
       }
@@ -1079,7 +1097,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e1.xbad = e2.xbad = b->xbad + l;
         ProfScope ps(CHM_K_EDGE_LAYER, s);
         HIPCHK(edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s));
-      } else if (b->l1_rows_a > 0 && m->edge16 && m->edge_split && !instrumented && !m->edge_trace) {
+      } else if (b->l1_rows_a > 0 && b->xbad && m->edge_split && !instrumented && !m->edge_trace) {
         // Edge layer 1 in whole rounds of the grid (rows [0, l1_rows_a)), then one grid with its
         // partial last round first and all of edge layer 2's segment tiles behind it (the few that
         // read those rows wait for them inside the grid). Same tiles, same arithmetic: bit-identical
@@ -1091,18 +1109,19 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e1b.row_base = b->l1_rows_a;
         e1b.flags = e2.flags = b->tail_flags;
         e1b.flag_row0 = e2.flag_row0 = b->l1_rows_a;
+        e2.xbad = b->xbad + 32 + l;  // (a timed-out wait: the repair launches recompute edge layer 2)
         HIPCHK(edge_gemm16(e1, EPI_EDGE, s));
-        HIPCHK(edge_gemm16_tail(e1b, e2, s));
+        HIPCHK(edge_gemm16_tail(e1b, e2, m->ncu, s));
       } else {
         {
           ProfScope ps(CHM_K_EDGE_FOURIER, s);
           HIPCHK(traced_edge_launch(m, e1, 1, E, s, [&] {
-            return m->edge16 ? edge_gemm16(e1, EPI_EDGE, s) : edge_gemm(e1, EPI_EDGE, s);
+            return edge_gemm16(e1, EPI_EDGE, s);
           }));
         }
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
         HIPCHK(traced_edge_launch(m, e2, 2, E, s, [&] {
-          return m->edge16 ? edge_gemm16(e2, EPI_SEGMEAN, s) : edge_gemm(e2, EPI_SEGMEAN, s);
+          return edge_gemm16(e2, EPI_SEGMEAN, s);
         }));
       }
     } else {

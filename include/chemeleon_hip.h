@@ -313,6 +313,22 @@ int chm_edge_features_split(chm_batch* b, const float* d_frac, void* d_split, vo
 int chm_prof_enable(int on);
 int chm_prof_reset(void);
 int chm_prof_read(int kernel, int64_t* launches, double* total_ms);
+/* Health counters of the edge kernels, counted on the device over every launch and graph replay
+ * since the last chm_prof_events_reset (synchronous device reads; not while capturing):
+ *   out[CHM_EV_LAYER_TIMEOUT]  k_edge16_layer: layer-2 tiles whose wait for their layer-1 tiles timed out
+ *   out[CHM_EV_LAYER_XCD]      k_edge16_layer: layer-2 tiles whose layer-1 tiles ran on another XCD
+ *   out[CHM_EV_LAYER_REPAIR]   k_edge16_layer launches recomputed by their repair pair
+ *   out[CHM_EV_TAIL_TIMEOUT]   k_edge16_tail: segment tiles whose wait for this grid's layer-1 tiles timed out
+ *   out[CHM_EV_TAIL_REPAIR]    k_edge16_tail launches whose edge layer 2 was recomputed
+ * Results never depend on these (a raised check is repaired before the layer's output is used); a
+ * non-zero count means the run paid for the repairs. n <= 8 values are written. */
+#define CHM_EV_LAYER_TIMEOUT 0
+#define CHM_EV_LAYER_XCD 1
+#define CHM_EV_LAYER_REPAIR 2
+#define CHM_EV_TAIL_TIMEOUT 3
+#define CHM_EV_TAIL_REPAIR 4
+int chm_prof_events(int64_t* out, int n);
+int chm_prof_events_reset(void);
 
 /* Sizes of the batch (for callers that allocate outputs). */
 int64_t chm_batch_num_nodes(const chm_batch* b);

@@ -303,7 +303,7 @@ def large_step_natoms(tag):
     raise KeyError(tag)
 
 
-LARGE_STEPS = (("256x40", [500]), ("64x40", [1000, 500, 1]), ("c4chunk256", [500]))
+LARGE_STEPS = (("256x40", [1000, 500, 2, 1]), ("64x40", [1000, 500, 1]), ("c4chunk256", [1000, 500, 2, 1]))
 
 
 def gen_large_steps(chm, csp):
@@ -520,7 +520,7 @@ def gen_clip_graph(chm, csp):
     save("clip_graph.npz", **rec)
 
 
-def _run_reference_trajectory(m, T, every):
+def _run_reference_trajectory(m, T, every, natoms=(6, 6, 6, 6), text="Li1 Mn1 O4", seed=42):
     from chemeleon.modules import schema
     states = []
     orig_get = schema.TrajectoryContainer.get_atoms
@@ -532,10 +532,11 @@ def _run_reference_trajectory(m, T, every):
 
     schema.TrajectoryContainer.get_atoms = get_atoms
     try:
-        torch.manual_seed(42)
+        torch.manual_seed(seed)
         last = None
-        for last in m._sample_generator([6] * 4, ["Li1 Mn1 O4"] * 4, 2.0, 1e-5):
-            pass
+        for k, last in enumerate(m._sample_generator(list(natoms), [text] * len(natoms), 2.0, 1e-5)):
+            if T >= 1000 and k % 50 == 0:
+                print(f"  reference trajectory {len(natoms)}x{natoms[0]}: step {k}/{T}", flush=True)
     finally:
         schema.TrajectoryContainer.get_atoms = orig_get
     keep = list(range(len(states) - 1, -1, -every))[::-1]  # always includes the final state (t = 0)
@@ -566,6 +567,18 @@ def gen_trajectory(chm, csp, T=100, every=1):
         extra = dict(atom_types_1thread=a1, frac_1thread=x1, lattices_1thread=lat1, threads=np.int64(nt))
     save(f"trajectory_4x6_T{T}.npz", atom_types=a, frac=x, lattices=lat, final_sorted_numbers=order_numbers,
          final_sorted_scaled=order_scaled, weights_crc=weights_crc(sd), t=ts, **extra)
+
+
+def gen_trajectory_64x20(chm, csp, every=50):
+    """configs[1]: 64 x 20 atoms ('Ti1 O2' composition text; the stub encoder returns the seeded
+    cond / null vectors), T = 1000, seed 42, the unmodified reference sampler (about 1 h of CPU).
+    Every `every`-th state and the final one are stored."""
+    T = 1000
+    m, sd = build_reference_model(chm, csp, T)
+    a, x, lat, keep, last = _run_reference_trajectory(m, T, every, natoms=[20] * 64, text="Ti1 O2", seed=42)
+    ts = np.array([T - 1 - k for k in keep])
+    save("trajectory_64x20_T1000.npz", atom_types=a.to(torch.uint8), frac=x, lattices=lat,
+         weights_crc=weights_crc(sd), t=ts, threads=np.int64(torch.get_num_threads()))
 
 
 def gen_state_keys(chm, csp):
@@ -652,7 +665,7 @@ if __name__ == "__main__":
     if not os.path.isdir(os.path.join(REF, "chemeleon")):
         print("reference not present; nothing to do")
         sys.exit(0)
-    torch.set_num_threads(8)
+    torch.set_num_threads(int(os.environ.get("CHM_GOLDEN_THREADS", "8")))
     chm, csp, du, sc = load_reference()
     which = sys.argv[1:] or ["schedules", "units", "decoder", "steps", "trajectory", "keys"]
     if "schedules" in which:
@@ -679,3 +692,5 @@ if __name__ == "__main__":
         gen_clip_graph(chm, csp)
     if "trajectory1000" in which:
         gen_trajectory(chm, csp, T=1000, every=10)
+    if "trajectory64x20" in which:
+        gen_trajectory_64x20(chm, csp)

@@ -262,6 +262,46 @@ def test_edge_tail_split_is_bit_identical(cn, nat):
         assert torch.equal(u, v), f"{what}: split and one-launch-per-layer edge schedules differ"
 
 
+def test_edge_tail_timeout_is_flagged_and_repaired(cn):
+    """k_edge16_tail's bounded waits (a segment tile reading rows of the grid's own layer-1 tiles) never
+    give a silent wrong answer: with the layer-1 tiles delayed ~10 ms and the waits shortened (option
+    'edge_tail_timeout'), the waits time out, the tiles raise the repair flag, the repair launches
+    recompute edge layer 2, and the step equals the one-launch-per-layer schedule bit for bit. The
+    device counters see the timeouts and repairs; without the repair ('edge_tail_norepair') the same
+    run gives different numbers, so the forced timeout really read unwritten S."""
+    nat = [40] * 64  # layer 1: 800 tiles on 256 CUs, a partial round of 32 -> the tail grid
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(13)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    model.decoder.set_option("edge_layer", 0)  # (the one-grid kernel would take this shape)
+    outs, events = [], []
+    for split, timeout, norepair in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)):
+        model.decoder.set_option("edge_split", split)
+        model.decoder.set_option("edge_tail_timeout", timeout)
+        model.decoder.set_option("edge_tail_norepair", norepair)
+        _lib.prof_events(reset=True)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+        torch.cuda.synchronize()
+        events.append(_lib.prof_events())
+    del model
+    torch.cuda.empty_cache()
+    print("events (two launches, tail, forced timeout, forced timeout without repair):", events)
+    assert events[0]["tail_wait_timeouts"] == 0 and events[1]["tail_wait_timeouts"] == 0
+    assert events[1]["tail_repairs"] == 0
+    assert events[2]["tail_wait_timeouts"] > 0 and events[2]["tail_repairs"] > 0
+    assert events[3]["tail_wait_timeouts"] > 0 and events[3]["tail_repairs"] == 0
+    for k, name in ((1, "tail grid"), (2, "tail grid, timed out + repaired")):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: {name} differs from one launch per layer"
+    assert not all(torch.equal(u, v) for u, v in zip(outs[0][1:], outs[3][1:])), \
+        "the forced timeout did not change the unrepaired result (the test would not see a missing repair)"
+
+
 @pytest.mark.parametrize("nat", [[40] * 64, [20] * 48, [80] * 9, [1] * 300 + [2] * 70 + [3] * 9,
                                  [23, 7, 40, 1, 80] * 23, [5, 9, 3, 12, 7, 1, 20]])
 def test_edge_row_tiles_are_bit_identical(cn, nat):
@@ -326,30 +366,6 @@ def test_one_grid_edge_layers_single_conditioning(cn):
         for k in (1, 2):
             for u, v in zip(outs[0], outs[k]):
                 assert torch.equal(u, v), f"one-grid (repair={k - 1}) differs from two launches, P = 1, B = {B}"
-    del model
-    torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("tag", ["64x20", "16x40"])
-def test_teacher_forced_steps_edge32_kernels(golden, cn, tag):
-    """The round-1 split16 edge kernels (v_mfma_f32_32x32x16_f16, k_edge_gemm; option edge16 = 0)
-    stay a tested arm: one step against the reference fixtures, same gates."""
-    model = _model(1000)
-    model.decoder.set_option("edge16", 0)
-    g = golden(f"step_{tag}.npz")
-    nat = g["natoms"].tolist()
-    B, N = len(nat), sum(nat)
-    for t in g["ts"][:2]:
-        t = int(t)
-        torch.manual_seed(5000 + t)
-        nz = None
-        if t > 1:
-            nz = (torch.rand((N, 104)), torch.randn(B, 3, 3), torch.randn(N, 3), torch.randn(N, 3))
-        a, x, lat = model.reverse_step(t, torch.from_numpy(g[f"t{t}_a"]), torch.from_numpy(g[f"t{t}_x"]),
-                                       torch.from_numpy(g[f"t{t}_l"]), nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)
-        np.testing.assert_array_equal(a.cpu().numpy(), g[f"t{t}_a_out"], err_msg=f"atom types t={t}")
-        periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"frac t={t}")
-        close(lat.cpu(), g[f"t{t}_l_out"], what=f"lattice t={t}")
     del model
     torch.cuda.empty_cache()
 

@@ -1,8 +1,7 @@
 // Standalone microbenchmark of the decoder GEMM kernels (edge shapes at 512x40).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DCHM_MICROBENCH tools/gemm_bench.cpp chemeleon_amd/csrc/kernels.hip \
-//         chemeleon_amd/csrc/gemm_bf16x3.hip chemeleon_amd/csrc/edge_gemm.hip chemeleon_amd/csrc/edge16.hip \
+//         chemeleon_amd/csrc/gemm_bf16x3.hip chemeleon_amd/csrc/split16.hip chemeleon_amd/csrc/edge16.hip \
 //         chemeleon_amd/csrc/node_gemm.hip -o tools/gemm_bench && tools/gemm_bench
-//   tools/gemm_bench 819200 768 edgecmp   # 32x32x16 vs 16x16x32 edge GEMM (EPI_STD), timing + agreement
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -75,40 +74,6 @@ int main(int argc, char** argv) {
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = K; g.A2 = A; g.lda2 = K; g.ksplit = K;
   g.W = W; g.ldw = K; g.C = C; g.ldc = N; g.bias = bias; g.act = 1; g.gb_rowmod = 1; g.Wp3 = W3;
   const double flops = 2.0 * M * N * K;
-  if (argc > 3 && std::string(argv[3]) == "edgecmp") {  // k_edge_gemm vs k_edge16, EPI_STD, same operands
-    void* W2h; float* wsc; _Float16* Ah; float* C2;
-    CK(hipMalloc(&W2h, 2L * N * K * 2)); CK(hipMalloc(&wsc, N * 4)); CK(hipMalloc(&Ah, 2L * (M + 256) * K * 2));
-    CK(hipMalloc(&C2, M * N * 4));
-    CK(split_rows_h(W, N, K, W2h, wsc, 0, s));
-    fill<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, 7, 1.9f);  // |A| < 1 like the Fourier features
-    split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
-    EdgeArgs ea{};
-    ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2h; ea.wscale = wsc; ea.C = C; ea.ldc = N;
-    EdgeArgs eb = ea;
-    eb.C = C2;
-    CK(edge_gemm(ea, EPI_STD, s));
-    CK(edge_gemm16(eb, EPI_STD, s));
-    CK(hipStreamSynchronize(s));
-    std::vector<float> h1(M * N), h2(M * N);
-    CK(hipMemcpy(h1.data(), C, M * N * 4, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(h2.data(), C2, M * N * 4, hipMemcpyDeviceToHost));
-    double mx = 0, rms = 0;
-    for (long i = 0; i < M * N; ++i) rms += (double)h1[i] * h1[i];
-    rms = std::sqrt(rms / (M * N));
-    for (long i = 0; i < M * N; ++i) mx = std::max(mx, (double)std::fabs(h1[i] - h2[i]) / std::max((double)std::fabs(h1[i]), rms));
-    printf("M=%ld K=%d: 16x16x32 vs 32x32x16 max scaled diff %.3e (rms %.3e)\n", M, K, mx, rms);
-    for (int rep = 0; rep < 3; ++rep) {
-      ea.C = C; eb.C = C2;
-      const float t1 = time_it(10, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
-      const float t2 = time_it(10, s, [&] { CK(edge_gemm16(eb, EPI_STD, s)); });
-      ea.C = nullptr; eb.C = nullptr;
-      const float t3 = time_it(10, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
-      const float t4 = time_it(10, s, [&] { CK(edge_gemm16(eb, EPI_STD, s)); });
-      printf("  32x32x16 %.3f ms %.1f TF (no C %.3f ms %.1f TF) | 16x16x32 %.3f ms %.1f TF (no C %.3f ms %.1f TF)\n", t1,
-             flops / t1 / 1e9, t3, flops / t3 / 1e9, t2, flops / t2 / 1e9, t4, flops / t4 / 1e9);
-    }
-    return 0;
-  }
   if (argc > 3 && std::string(argv[3]) == "edge") {  // glds edge GEMM only (PMC runs); "edge0" = no C stores
     void* W2h; float* wsc; _Float16* Ah;
     CK(hipMalloc(&W2h, 2L * N * K * 2)); CK(hipMalloc(&wsc, N * 4)); CK(hipMalloc(&Ah, 2L * M * K * 2));
@@ -116,20 +81,14 @@ int main(int argc, char** argv) {
     split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
     EdgeArgs ea{};
     ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2h; ea.wscale = wsc; ea.C = C; ea.ldc = N;
-    float te = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    float te = time_it(5, s, [&] { CK(edge_gemm16(ea, EPI_STD, s)); });
     ea.C = nullptr;
-    float t0 = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    float t0 = time_it(5, s, [&] { CK(edge_gemm16(ea, EPI_STD, s)); });
     printf("M=%ld K=%d glds edge GEMM: %.3f ms %.1f TF fp32-eq; without C stores %.3f ms %.1f TF\n", M, K, te,
            flops / te / 1e9, t0, flops / t0 / 1e9);
-    ea.C = nullptr;
-    for (int rep = 0; rep < 3; ++rep)
-      for (int var : {0, 3, 5, 7}) {
-        float tv = time_it(5, s, [&] { CK(edge_gemm_variant(ea, var, s)); });
-        printf("  variant %d (no C): %.3f ms %.1f TF\n", var, tv, flops / tv / 1e9);
-      }
     for (int dbg = 1; dbg < 4; ++dbg) {
       ea.dbg = dbg;
-      float td = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+      float td = time_it(5, s, [&] { CK(edge_gemm16(ea, EPI_STD, s)); });
       printf("  ablation %d (%s%s): %.3f ms %.1f TF\n", dbg, dbg & 1 ? "no loop loads " : "", dbg & 2 ? "no barriers" : "",
              td, flops / td / 1e9);
     }
@@ -148,20 +107,20 @@ int main(int argc, char** argv) {
     split_h<<<(M * K + 255) / 256, 256, 0, s>>>(A, M * K, Ah);
     EdgeArgs ea{};
     ea.M = M; ea.N = N; ea.K = K; ea.A = Ah; ea.W = W2r; ea.wscale = wsc; ea.C = C; ea.ldc = N;
-    float te = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+    float te = time_it(5, s, [&] { CK(edge_gemm16(ea, EPI_STD, s)); });
     printf("  glds edge GEMM: %.3f ms %.1f TF fp32-equivalent\n", te, flops / te / 1e9);
     std::vector<float> c1(65536 * 4), c2(65536 * 4);
     GemmArgs gp = g; gp.bias = nullptr; gp.act = 0;
     CK(gemm(gp, EPI_STD, s)); CK(hipStreamSynchronize(s));
     CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
-    CK(edge_gemm(ea, EPI_STD, s)); CK(hipStreamSynchronize(s));
+    CK(edge_gemm16(ea, EPI_STD, s)); CK(hipStreamSynchronize(s));
     CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
     double mx = 0, ref = 0;
     for (size_t i = 0; i < c1.size(); ++i) { mx = fmax(mx, fabs((double)c1[i] - c2[i])); ref = fmax(ref, fabs((double)c1[i])); }
     printf("  max |edge - f32mfma| = %.3e (max |C| %.3e)\n", mx, ref);
     if (K % 128 == 0 && K <= 512) {
       ea.aexp = aexp;
-      float ta = time_it(5, s, [&] { CK(edge_gemm(ea, EPI_STD, s)); });
+      float ta = time_it(5, s, [&] { CK(edge_gemm16(ea, EPI_STD, s)); });
       CK(hipMemcpy(c2.data(), C, c2.size() * 4, hipMemcpyDeviceToHost));
       mx = 0;
       for (size_t i = 0; i < c1.size(); ++i) mx = fmax(mx, fabs((double)c1[i] - c2[i]));

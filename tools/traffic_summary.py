@@ -1,46 +1,19 @@
-"""Per-launch HBM traffic per kernel from the two PMC passes of tools/pmc_traffic.sh.
-
-FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
-coalesced streaming reads (MI355X_MICROARCH.md, HBM section), so it is doubled here.
-Usage: python tools/traffic_summary.py gpurun_out/traffic > profiles/r1/traffic.json
+"""Per-launch HBM traffic per kernel from the two PMC passes of tools/pmc_traffic.sh
+(FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE; chemeleon_amd/pmc.py), with the box it ran on.
+Usage: python tools/traffic_summary.py gpurun_out/traffic > profiles/rN/traffic.json
+(run on the GPU box, so that `box` names the machine the counters came from)
 """
-import collections
-import csv
-import glob
 import json
+import os
 import sys
 
-
-def per_kernel(path, counter):
-    vals = collections.defaultdict(list)
-    for f in glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
-        per_dispatch = collections.defaultdict(float)
-        names = {}
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            per_dispatch[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            names[r["Dispatch_Id"]] = r["Kernel_Name"]
-        for d, v in per_dispatch.items():
-            vals[names[d]].append(v * 1024.0)
-    return vals
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from chemeleon_amd.pmc import box_id, traffic  # noqa: E402
 
 
 def main(path):
-    fetch = per_kernel(path + "/fetch", "FETCH_SIZE")
-    write = per_kernel(path + "/write", "WRITE_SIZE")
-    out = {}
-    for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        if not f and not w:
-            continue
-        fb = 2.0 * sum(f) / len(f) if f else None
-        wb = sum(w) / len(w) if w else None
-        out[k] = {"launches": max(len(f), len(w)), "read_bytes": fb, "write_bytes": wb,
-                  "bytes_per_launch": (fb or 0.0) + (wb or 0.0)}
     json.dump({"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, bytes per launch, averaged",
-               "kernels": out}, sys.stdout, indent=1)
+               "box": box_id(), "kernels": traffic(path + "/fetch", path + "/write")}, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
