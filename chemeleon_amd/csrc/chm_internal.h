@@ -141,7 +141,11 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s);
 // g2.xbad: raised on a timed-out wait; the repair launches behind the grid then recompute layer 2
 hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_grid, hipStream_t s);
 // both edge layers in one grid (row tiles; layer-2 tiles of row tile i - lag behind layer 1's row tile i)
-hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s);
+// sched != null: the persistent form (grid blocks; the last pool% of the row tiles claimed at run time;
+// sched = the layer's zeroed scheduling words, 16 + 8 * cap, cap >= R + lag + 64)
+hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s,
+                             unsigned* sched = nullptr, int cap = 0, int grid = 0, int pool = 15);
+void edge16_seq_jobs(long n, int P, int D, long* out);  // (host) the persistent form's job sequence of one XCD
 long edge16_layer_blocks(long R, int P);                        // its grid size
 void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map
 hipError_t edge16_init();

@@ -101,9 +101,11 @@ __host__ __device__ inline LayerJob layer_job(long b, long R, int P, int D) {
 // the flag word and a layer-2 tile that finds another one raises *xbad (the runtime's repair launches
 // then recompute the layer).
 template <int EPI, bool ASC, bool ONE = false>
-__device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb, long bid_in = -1) {
+__device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb, long bid_in = -1, int tid_in = -1) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // (tid_in >= 0: the persistent kernel's opaque copy of threadIdx.x, so its loop does not hoist the
+  // tile's index math out of the loop and keep it in registers)
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int l16 = lane & 15, g4 = lane >> 4;
   const int ntn = g.N / BN;
@@ -234,6 +236,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         __hip_atomic_store(f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    stamp(4);  // (traces of this grid: slot 4 = the wait for the layer-1 tiles is over)
   }
 
   // ---- row exponents of the A chunks (edge layer 2): the lane's four rows
@@ -686,9 +689,9 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
-    stamp(4);
+    if (!ONE) stamp(4);
     for (int half = 0; half < 2; ++half) {
-      if (half == 1) stamp(5);
+      if (half == 1 && !ONE) stamp(5);
       if (wn == half) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -841,6 +844,115 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer(EdgeArgs g1, EdgeArgs g
     edge16_tile<EPI_SEGMEAN, true, true>(g2, blockIdx.x, gridDim.x, j.bid);
 }
 
+// The persistent form of k_edge16_layer (option edge_layer_dyn, the default): one block per CU, each
+// looping over jobs of its XCD's sequence. The sequence has the static map's group structure (layer-1
+// tiles of local row i interleaved with the layer-2 tiles of local row i - D; seq_job), but the global
+// row tile behind a local row is claimed at run time from one counter shared by all XCDs, so an XCD
+// that runs faster claims more rows (the static map gives every XCD R / 8 rows, and the slowest XCD
+// then sets the launch time: 5% at 512x40, traces in profiles/r3/). Per layer and launch (zeroed per
+// decoder call): sched[x] the jobs taken on XCD x, sched[8] the rows claimed, and the slots
+// sched[16 + x * cap + i] of XCD x's local rows (0 = not yet resolved, row + 1, or ~0u = no row).
+// Claims go in local-row order (the claim of row i waits for row i-1's), so each XCD's valid rows are
+// a prefix 0 .. n_x - 1: a block that takes a layer-2 job of an invalid row knows every later job of
+// its XCD is invalid and exits; a layer-1 job of an invalid row is skipped. Every wait is for a job
+// taken earlier by a running block (deadlock-free whatever the residency), and bounded: a timed-out
+// wait raises the layer's repair request.
+struct SeqJob { int kind; long row; int sub; };  // kind 1: layer 1 (sub = column tile), 2: layer 2 (sub = cond * 2 + col)
+__host__ __device__ inline SeqJob seq_job(long k, int P, int D) {
+  const long G = 2 + 2L * P;
+  if (k < 2L * D) return SeqJob{1, k / 2, (int)(k % 2)};
+  const long q = k - 2L * D, i = D + q / G;
+  const int sub = (int)(q % G);
+  if (sub < 2) return SeqJob{1, i, sub};
+  return SeqJob{2, i - D, sub - 2};
+}
+
+namespace {
+__device__ __forceinline__ unsigned wait_slot(const unsigned* p, bool& late) {
+  unsigned v, spins = 0;
+  while ((v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u && spins < (1u << 20)) {
+    ++spins;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (v == 0u) late = true;
+  return v;
+}
+}  // namespace
+
+// Rows: XCD x owns the static rows [x ns, (x + 1) ns) as its local rows 0 .. ns - 1 (no lookup), the
+// rest of the grid's row tiles, [8 ns, R), form the shared pool its local rows ns, ns + 1, ... claim
+// from. A static row costs a job only the XCD counter's atomic (about what the hardware dispatcher of
+// the static map costs per block); the pool absorbs the XCDs' different speeds at the end.
+__global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeArgs g2, int R, int D, unsigned* sched,
+                                                             int cap, int ns) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const unsigned x = xcc_id();
+  const int P = g2.npairs;
+  unsigned* slots = sched + 16 + (long)x * cap;  // local row ns + i -> slots[i]
+  int* bc = reinterpret_cast<int*>(lds);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const long k = (long)__hip_atomic_fetch_add(sched + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const SeqJob j = seq_job(k, P, D);
+      int code = 0;  // 0 = exit, 1 = layer 1, 2 = layer 2, 3 = skip
+      unsigned v = 0;  // the row + 1, ~0u = none
+      bool late = false;
+      const long jd = j.row - ns;  // pool slot of a local row past the static ones
+      if (jd >= cap) {
+        v = ~0u;  // (beyond every possible row: its layer-2 row is invalid too)
+      } else if (jd < 0) {
+        v = (unsigned)(x * ns + j.row) + 1u;
+      } else if (j.kind == 1 && j.sub == 0) {  // claim, after the previous local row's claim (valid rows: a prefix)
+        const unsigned prev = jd > 0 ? wait_slot(slots + jd - 1, late) : 1u;
+        v = ~0u;
+        if (prev != ~0u && prev != 0u) {
+          const unsigned r = (unsigned)(8 * ns) + __hip_atomic_fetch_add(sched + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (r < (unsigned)R) v = r + 1u;
+        }
+        __hip_atomic_store(slots + jd, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        v = wait_slot(slots + jd, late);
+        if (v == 0u) v = ~0u;
+      }
+      long bid = 0;
+      if (j.kind == 1) {
+        code = v == ~0u ? 3 : 1;
+        bid = (long)(v - 1u) * 2 + j.sub;
+      } else {
+        code = v == ~0u ? 0 : 2;
+        bid = ((long)(v - 1u) * P + j.sub / 2) * 2 + (j.sub & 1);
+      }
+      if (late) {  // (never in a healthy run: the layer is recomputed by the repair launches)
+        __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        count_event(EV_LAYER_TIMEOUT);
+      }
+      bc[0] = code;
+      bc[1] = (int)bid;
+      bc[2] = (int)(8 * k + x);
+    }
+    __syncthreads();
+    const int code = bc[0], bid = bc[1], vb = bc[2];
+    __syncthreads();
+    if (code == 0) break;
+    if (code == 3) continue;  // (a layer-1 job of a row past the end: no tile)
+    // (the tiles read their arguments through laundered kernarg pointers: otherwise the compiler keeps
+    // both argument blocks in SGPRs across the loop and spills them)
+    typedef const __attribute__((address_space(4))) char* kptr;
+    kptr kp = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    constexpr long off2 = (sizeof(EdgeArgs) + alignof(EdgeArgs) - 1) / alignof(EdgeArgs) * alignof(EdgeArgs);
+    const EdgeArgs* a1 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)kp;
+    const EdgeArgs* a2 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)(kp + off2);
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    if (code == 1)
+      edge16_tile<EPI_EDGE, false, true>(*a1, vb, 0, bid, tid);
+    else
+      edge16_tile<EPI_SEGMEAN, true, true>(*a2, vb, 0, bid, tid);
+    __syncthreads();
+  }
+}
+
 // Repair of a k_edge16_layer launch whose check failed (*g.xbad != 0: some layer-2 tile read S written
 // on another XCD, so its L2 view may have been stale): one layer on the two-launch schedule, grid-
 // stride over the tiles so that the normal case (nothing to repair) costs one small grid that exits.
@@ -864,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, 
 hipError_t edge16_init() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
-                      (const void*)k_edge16_tail, (const void*)k_edge16_layer,
+                      (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
@@ -931,7 +1043,17 @@ void edge16_layer_jobs(long R, int P, int D, long* out) {
   }
 }
 
-hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s) {
+void edge16_seq_jobs(long n, int P, int D, long* out) {
+  for (long k = 0; k < n; ++k) {
+    const SeqJob j = seq_job(k, P, D);
+    out[3 * k] = j.kind;
+    out[3 * k + 1] = j.row;
+    out[3 * k + 2] = j.sub;
+  }
+}
+
+hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s,
+                             unsigned* sched, int cap, int grid, int pool) {
   if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
       !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.row_base != 0 || g1.flags || !g1.lflags ||
       !g1.xbad || g1.xbad != g2.xbad)
@@ -948,8 +1070,15 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
     attr = true;
   }
   const long R = g2.ntiles;
-  const long blocks = edge16_layer_blocks(R, g2.npairs);
-  hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
+  if (sched) {  // persistent, the last rows claimed at run time (k_edge16_layer_dyn)
+    if (grid < 1 || cap < R + lag + 64 || pool < 0 || pool > 100) return hipErrorInvalidValue;
+    const int ns = (int)((R - (R * pool + 99) / 100) / 8);  // static rows per XCD
+    hipLaunchKernelGGL(k_edge16_layer_dyn, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, (int)R, lag, sched, cap,
+                       ns);
+  } else {
+    const long blocks = edge16_layer_blocks(R, g2.npairs);
+    hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the repair pair (exits at once unless a layer-2 tile flagged another XCD's layer-1 tile)

@@ -50,6 +50,7 @@ constexpr int kMaxTailTiles = 512;  // layer-1 row tiles of a partial round (< C
 // k_edge16_layer only from 256 row tiles (32 per XCD) on: 64x20 (100 row tiles, 12-13 per XCD, mostly
 // inside the layer-2 lag) measured 0.186 vs 0.176 ms for the two launches; 64x40 (400) gains 5%
 constexpr long kLayerMinTiles = 256;
+constexpr int kMaxLag = 1000;  // edge_lag's upper bound (sizes the persistent one-grid kernel's row slots)
 
 struct chm_model {
   chm_dims d;
@@ -71,10 +72,12 @@ struct chm_model {
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
   int edge_lag = 10;     // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD
+  int edge_dyn = 1;      // CHM_EDGE_DYN=0: the one-grid kernel with the static block -> job map (k_edge16_layer)
+  int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int ncu = 0;           // compute units of the device the model lives on
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
-  int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2
+  int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2 (two-launch schedule), 3 (k_edge16_layer)
   std::vector<LayerW> layers;
 };
 
@@ -97,6 +100,8 @@ struct chm_batch {
   unsigned* rcnt = nullptr;
   unsigned* lflags = nullptr;  // k_edge16_layer: per row tile (returns to 0 at the end of every launch)
   unsigned* xbad = nullptr;    // k_edge16_layer: per layer, raised when its repair launches must run
+  unsigned* sched = nullptr;   // k_edge16_layer_dyn: per layer 16 + 8 * sched_cap words, zeroed per decoder call
+  long sched_cap = 0;
   int math;     // arithmetic mode fixed at creation (copied from the model)
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
@@ -284,6 +289,10 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (lay) m->edge_layer = atoi(lay);
     const char* lag = getenv("CHM_EDGE_LAG");
     if (lag) m->edge_lag = atoi(lag) > 0 ? atoi(lag) : 1;
+    const char* dyn = getenv("CHM_EDGE_DYN");
+    if (dyn) m->edge_dyn = atoi(dyn);
+    const char* pool = getenv("CHM_EDGE_POOL");
+    if (pool) m->edge_pool = atoi(pool);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -396,8 +405,17 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_layer = value != 0;
     return CHM_OK;
   }
+  if (k == "edge_layer_dyn") {  // persistent one-grid kernel, rows claimed at run time; bit-identical
+    m->edge_dyn = value != 0;
+    return CHM_OK;
+  }
+  if (k == "edge_pool") {  // its run-time-claimed share of the row tiles, percent (0: static rows only)
+    if (value < 0 || value > 100) return fail(CHM_E_ARG, "edge_pool must be in [0, 100]");
+    m->edge_pool = (int)value;
+    return CHM_OK;
+  }
   if (k == "edge_lag") {
-    if (value < 1 || value > 1000) return fail(CHM_E_ARG, "edge_lag must be in [1, 1000]");
+    if (value < 1 || value > kMaxLag) return fail(CHM_E_ARG, "edge_lag must be in [1, 1000]");
     m->edge_lag = (int)value;
     return CHM_OK;
   }
@@ -610,6 +628,8 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->rcnt = (unsigned*)carve((size_t)P * b->nrt * 8 * sizeof(unsigned));
     b->lflags = (unsigned*)carve(b->nrt * sizeof(unsigned));
     b->xbad = (unsigned*)carve(64 * sizeof(unsigned));
+    b->sched_cap = b->nrt + kMaxLag + 64;
+    b->sched = (unsigned*)carve((size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned));
   }
   if (b->knn) {  // (E = the edge capacity E_cap)
     b->cand_off = (long*)carve((B + 1) * sizeof(long));
@@ -738,6 +758,12 @@ extern "C" int64_t chm_debug_layer_jobs(int64_t R, int P, int lag, int64_t* out,
   const long nb = edge16_layer_blocks(R, P);
   if (out && cap >= 2 * nb) edge16_layer_jobs(R, P, lag, reinterpret_cast<long*>(out));
   return nb;
+}
+
+extern "C" int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out) {
+  if (n < 0 || P < 1 || P > 2 || lag < 1 || !out) return fail(CHM_E_ARG, "bad arguments");
+  edge16_seq_jobs(n, P, lag, reinterpret_cast<long*>(out));
+  return CHM_OK;
 }
 
 extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
@@ -931,7 +957,7 @@ static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which
                   hipStreamIsCapturing(s, &cst) == hipSuccess && cst == hipStreamCaptureStatusNone && ++traced == 4;
   if (!tr) return launch();
   unsigned long long* tbuf = nullptr;
-  const long tblocks = 4 * (E / 128 + 1) + 4096;
+  const long tblocks = (which == 3 ? 48 * (E / 256 + 1) : 4 * (E / 128 + 1)) + 4096;  // (3: slot 8 k + XCD)
   hipError_t e = hipMalloc(&tbuf, tblocks * 48);
   if (e == hipSuccess) e = hipMemsetAsync(tbuf, 0, tblocks * 48, s);
   if (e != hipSuccess) return e;
@@ -1043,6 +1069,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)
     HIPCHK(hipMemsetAsync(b->xbad, 0, 64 * sizeof(unsigned), s));
+    if (m->edge_rows && m->edge_layer && m->edge_dyn)
+      HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
@@ -1091,12 +1119,22 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (e2.rtiles && m->edge_layer && b->nrt >= kLayerMinTiles && !m->edge_trace) {
+      if (e2.rtiles && m->edge_layer && b->nrt >= kLayerMinTiles && (!m->edge_trace || m->edge_trace_layer == 3)) {
         // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
         e1.lflags = e2.lflags = b->lflags;
         e1.xbad = e2.xbad = b->xbad + l;
         ProfScope ps(CHM_K_EDGE_LAYER, s);
-        HIPCHK(edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s));
+        // (CHM_EDGE_TRACE_LAYER=3: block timelines of this grid, slot = blockIdx)
+        HIPCHK(traced_edge_launch(m, e1, 3, E, s, [&] {
+          e2.trace = e1.trace;
+          const hipError_t r =
+              m->edge_dyn && m->ncu > 0
+                  ? edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s, b->sched + (size_t)l * (16 + 8 * b->sched_cap),
+                                      (int)b->sched_cap, m->ncu, m->edge_pool)
+                  : edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s);
+          e2.trace = nullptr;
+          return r;
+        }));
       } else if (b->l1_rows_a > 0 && b->xbad && m->edge_split && !instrumented && !m->edge_trace) {
         // Edge layer 1 in whole rounds of the grid (rows [0, l1_rows_a)), then one grid with its
         // partial last round first and all of edge layer 2's segment tiles behind it (the few that
