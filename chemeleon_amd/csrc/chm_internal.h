@@ -145,7 +145,7 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_g
 // sched = the layer's zeroed scheduling words, 16 + 8 * cap, cap >= R + lag + 64)
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s,
                              unsigned* sched = nullptr, int cap = 0, int grid = 0, int pool = 15);
-void edge16_seq_jobs(long n, int P, int D, long* out);  // (host) the persistent form's job sequence of one XCD
+void edge16_seq_jobs(long n, int P, int D, long* out);  // (host) the persistent form's per-XCD job sequence
 long edge16_layer_blocks(long R, int P);                        // its grid size
 void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map
 hipError_t edge16_init();

@@ -844,20 +844,27 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer(EdgeArgs g1, EdgeArgs g
     edge16_tile<EPI_SEGMEAN, true, true>(g2, blockIdx.x, gridDim.x, j.bid);
 }
 
-// The persistent form of k_edge16_layer (option edge_layer_dyn, the default): one block per CU, each
-// looping over jobs of its XCD's sequence. The sequence has the static map's group structure (layer-1
-// tiles of local row i interleaved with the layer-2 tiles of local row i - D; seq_job), but the global
-// row tile behind a local row is claimed at run time from one counter shared by all XCDs, so an XCD
-// that runs faster claims more rows (the static map gives every XCD R / 8 rows, and the slowest XCD
-// then sets the launch time: 5% at 512x40, traces in profiles/r3/). Per layer and launch (zeroed per
-// decoder call): sched[x] the jobs taken on XCD x, sched[8] the rows claimed, and the slots
-// sched[16 + x * cap + i] of XCD x's local rows (0 = not yet resolved, row + 1, or ~0u = no row).
-// Claims go in local-row order (the claim of row i waits for row i-1's), so each XCD's valid rows are
-// a prefix 0 .. n_x - 1: a block that takes a layer-2 job of an invalid row knows every later job of
-// its XCD is invalid and exits; a layer-1 job of an invalid row is skipped. Every wait is for a job
-// taken earlier by a running block (deadlock-free whatever the residency), and bounded: a timed-out
-// wait raises the layer's repair request.
+// The persistent form of k_edge16_layer (option edge_layer_dyn; the default from kDynMinTiles row tiles
+// on): one block per CU, each looping over jobs of its XCD's sequence (an atomic per job on the XCD's
+// counter). The sequence has the static map's group structure (layer-1 tiles of local row i interleaved
+// with the layer-2 tiles of local row i - D; seq_job). XCD x's first ns local rows are its static rows
+// x ns .. (x + 1) ns - 1; the rest of the grid's row tiles, [8 ns, R) (edge_pool percent), form a pool
+// its later local rows claim from at run time through one counter shared by all XCDs, so an XCD that
+// runs faster claims more of them (with the static map every XCD gets R / 8 rows and the slowest one
+// sets the launch time: the XCDs' last blocks ended 240 us apart in a 4.8 ms launch at 512x40,
+// profiles/r3/traces). Per layer and launch (zeroed per decoder call): sched[x] the jobs taken on XCD x,
+// sched[8] the pool rows claimed, and the slots sched[16 + x * cap + i] of XCD x's pool rows (0 = not
+// yet resolved, row + 1, or ~0u = no row). Claims go in local-row order (the claim of row i waits for
+// row i-1's), so each XCD's valid rows are a prefix: a block that takes a layer-2 job of an invalid row
+// knows every later job of its XCD is invalid and exits; a layer-1 job of an invalid row is skipped.
+// Every wait is for a job taken earlier by a running block (deadlock-free whatever the residency), and
+// bounded: a timed-out wait raises the layer's repair request.
 struct SeqJob { int kind; long row; int sub; };  // kind 1: layer 1 (sub = column tile), 2: layer 2 (sub = cond * 2 + col)
+// Job k of an XCD's sequence: the first 2D jobs are the layer-1 tiles of local rows 0 .. D-1, then groups
+// i = D, D+1, ... of [layer 1 of row i (2 jobs), layer 2 of row i - D (2P)] (the static map's pattern,
+// unbounded). Measured and not kept: the pool rows' layer-1 tiles running ahead twice as fast (so
+// that a backlog of layer-2 tiles covers the last row's layer-1 + layer-2 chain at the end): 512x40
+// 59.2 -> 60.6 ms per step (profiles/r3/ab_runahead.txt).
 __host__ __device__ inline SeqJob seq_job(long k, int P, int D) {
   const long G = 2 + 2L * P;
   if (k < 2L * D) return SeqJob{1, k / 2, (int)(k % 2)};
@@ -879,10 +886,9 @@ __device__ __forceinline__ unsigned wait_slot(const unsigned* p, bool& late) {
 }
 }  // namespace
 
-// Rows: XCD x owns the static rows [x ns, (x + 1) ns) as its local rows 0 .. ns - 1 (no lookup), the
-// rest of the grid's row tiles, [8 ns, R), form the shared pool its local rows ns, ns + 1, ... claim
-// from. A static row costs a job only the XCD counter's atomic (about what the hardware dispatcher of
-// the static map costs per block); the pool absorbs the XCDs' different speeds at the end.
+// (A static row's job costs only the XCD counter's atomic, about what the hardware dispatch of a block
+// of the static map costs; claiming every row from the pool measured slower: 512x40 58.15 vs 57.9 ms
+// per step at edge_pool 30 vs 15.)
 __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeArgs g2, int R, int D, unsigned* sched,
                                                              int cap, int ns) {
   extern __shared__ __attribute__((aligned(16))) char lds[];

@@ -50,7 +50,11 @@ constexpr int kMaxTailTiles = 512;  // layer-1 row tiles of a partial round (< C
 // k_edge16_layer only from 256 row tiles (32 per XCD) on: 64x20 (100 row tiles, 12-13 per XCD, mostly
 // inside the layer-2 lag) measured 0.186 vs 0.176 ms for the two launches; 64x40 (400) gains 5%
 constexpr long kLayerMinTiles = 256;
-constexpr int kMaxLag = 1000;  // edge_lag's upper bound (sizes the persistent one-grid kernel's row slots)
+constexpr int kMaxLag = 1000;
+// the persistent one-grid kernel from this many row tiles on (same-box A/B, profiles/r3/ab_*: 512x40 (3200)
+// 60.2 -> 59.2 ms per step; 64x40 (400) 8.34 -> 8.44: the per-job atomic costs more than the XCD
+// balancing gains in a short grid)
+constexpr long kDynMinTiles = 1024;  // edge_lag's upper bound (sizes the persistent one-grid kernel's row slots)
 
 struct chm_model {
   chm_dims d;
@@ -72,7 +76,8 @@ struct chm_model {
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
   int edge_lag = 10;     // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD
-  int edge_dyn = 1;      // CHM_EDGE_DYN=0: the one-grid kernel with the static block -> job map (k_edge16_layer)
+  int edge_dyn = 1;      // CHM_EDGE_DYN: one-grid kernel form, 0 static block -> job map (k_edge16_layer), 1 the
+                         // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int ncu = 0;           // compute units of the device the model lives on
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
@@ -405,8 +410,9 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_layer = value != 0;
     return CHM_OK;
   }
-  if (k == "edge_layer_dyn") {  // persistent one-grid kernel, rows claimed at run time; bit-identical
-    m->edge_dyn = value != 0;
+  if (k == "edge_layer_dyn") {  // persistent one-grid kernel: 0 never, 1 from kDynMinTiles row tiles on, 2 always
+    if (value < 0 || value > 2) return fail(CHM_E_ARG, "edge_layer_dyn must be 0, 1 or 2");
+    m->edge_dyn = (int)value;
     return CHM_OK;
   }
   if (k == "edge_pool") {  // its run-time-claimed share of the row tiles, percent (0: static rows only)
@@ -1069,7 +1075,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)
     HIPCHK(hipMemsetAsync(b->xbad, 0, 64 * sizeof(unsigned), s));
-    if (m->edge_rows && m->edge_layer && m->edge_dyn)
+    if (m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
   }
@@ -1128,7 +1134,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         HIPCHK(traced_edge_launch(m, e1, 3, E, s, [&] {
           e2.trace = e1.trace;
           const hipError_t r =
-              m->edge_dyn && m->ncu > 0
+              m->ncu > 0 && (m->edge_dyn == 2 || (m->edge_dyn == 1 && b->nrt >= kDynMinTiles))
                   ? edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s, b->sched + (size_t)l * (16 + 8 * b->sched_cap),
                                       (int)b->sched_cap, m->ncu, m->edge_pool)
                   : edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s);

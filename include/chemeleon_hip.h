@@ -285,10 +285,10 @@ int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t c
  * tile index (layer 1: row tile * 2 + column tile; layer 2: (row tile * P + conditioning) * 2 +
  * column tile)}. */
 int64_t chm_debug_layer_jobs(int64_t R, int P, int lag, int64_t* out, int64_t cap);
-/* The persistent form of that kernel (option edge_layer_dyn, the default): job k of an XCD's sequence
- * as out[3k] = kind (1 = layer 1, 2 = layer 2), out[3k+1] = the XCD's local row (mapped to a global row
- * tile when the kernel claims it), out[3k+2] = column tile (layer 1) or conditioning * 2 + column tile
- * (layer 2), for k < n. */
+/* The persistent form of that kernel (option edge_layer_dyn, the default from 1024 row tiles on): job k
+ * of an XCD's sequence as out[3k] = kind (1 = layer 1, 2 = layer 2), out[3k+1] = the XCD's local row
+ * (the first ones its static rows, the rest claimed from the shared pool at run time), out[3k+2] =
+ * column tile (layer 1) or conditioning * 2 + column tile (layer 2), for k < n. */
 int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out);
 
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):

@@ -325,9 +325,9 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
     model = _model(1000)
     outs = []
     _lib.prof_events(reset=True)
-    for rows, nowait, layer, lag, repair, dyn in ((0, 0, 0, 10, 0, 1), (1, 0, 0, 10, 0, 1), (1, 1, 0, 10, 0, 1),
-                                                  (1, 0, 0, 10, 0, 1), (1, 0, 1, 10, 0, 1), (1, 0, 1, 1, 0, 1),
-                                                  (1, 1, 1, 3, 0, 1), (1, 0, 1, 10, 1, 1), (1, 0, 1, 10, 0, 0),
+    for rows, nowait, layer, lag, repair, dyn in ((0, 0, 0, 10, 0, 2), (1, 0, 0, 10, 0, 2), (1, 1, 0, 10, 0, 2),
+                                                  (1, 0, 0, 10, 0, 2), (1, 0, 1, 10, 0, 2), (1, 0, 1, 1, 0, 2),
+                                                  (1, 1, 1, 3, 0, 2), (1, 0, 1, 10, 1, 2), (1, 0, 1, 10, 0, 0),
                                                   (1, 0, 1, 2, 0, 0), (1, 0, 1, 10, 1, 0)):
         model.decoder.set_option("edge_rows", rows)
         model.decoder.set_option("edge_rows_nowait", nowait)
@@ -365,7 +365,7 @@ def test_one_grid_edge_layers_single_conditioning(cn):
         te = model.time_embed(torch.full((B,), 300, dtype=torch.long)).to(DEV)
         nat_t = torch.tensor(nat)
         outs = []
-        for layer, repair, dyn in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, 0, 0)):
+        for layer, repair, dyn in ((0, 0, 2), (1, 0, 2), (1, 1, 2), (1, 0, 0)):
             model.decoder.set_option("edge_layer", layer)
             model.decoder.set_option("edge_layer_repair", repair)
             model.decoder.set_option("edge_layer_dyn", dyn)

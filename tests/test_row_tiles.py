@@ -109,30 +109,27 @@ def test_layer_grid_schedule(R, P, lag):
 @pytest.mark.parametrize("P,lag", [(2, 10), (1, 10), (2, 1), (2, 3), (1, 4)])
 def test_persistent_layer_sequence(P, lag):
     """The persistent one-grid kernel's per-XCD job sequence (chm_debug_layer_seq, the function the
-    kernel runs): every local row gets its 2 layer-1 tiles and its 2 P layer-2 tiles exactly once, and
-    every layer-2 job of a row comes after both of that row's layer-1 jobs (the claim of the row's
-    global tile happens at its first layer-1 job, so a layer-2 job's wait always points to jobs taken
-    earlier). Also the kernel's exit rule: once a layer-2 job's row is past the last valid row, every
-    later job's layer-2 row is too."""
-    n = 4000
+    kernel runs): every local row gets its 2 layer-1 tiles and its 2 P layer-2 tiles exactly once, column tile 0 of a row
+    (the job that claims a pool row) comes before its column tile 1, every layer-2 job of a row comes
+    after both of that row's layer-1 jobs (a layer-2 job's waits always point to jobs taken earlier),
+    and layer-2 rows never go back (the kernel's exit rule: once a layer-2 job's row is past the last
+    valid row, so is every later job's)."""
+    n = 6000
     out = (ctypes.c_int64 * (3 * n))()
     assert _lib.load().chm_debug_layer_seq(n, P, lag, out) == 0
     jobs = [tuple(out[3 * k:3 * k + 3]) for k in range(n)]
     seen = {}
-    first_l1 = {}
     for k, (kind, row, sub) in enumerate(jobs):
         assert (kind, row, sub) not in seen
         seen[(kind, row, sub)] = k
         if kind == 1:
             assert sub in (0, 1)
-            first_l1.setdefault(row, k)
             if sub == 1:
-                assert seen[(1, row, 0)] < k  # the claim (column tile 0) comes first
+                assert seen[(1, row, 0)] < k
         else:
-            assert kind == 2 and 0 <= sub < 2 * P
+            assert kind == 2 and 0 <= sub < 2 * P and row >= 0
             assert seen[(1, row, 0)] < k and seen[(1, row, 1)] < k
     rows2 = [row for kind, row, _ in jobs if kind == 2]
-    assert rows2 == sorted(rows2)  # layer-2 rows never go back: the exit rule holds
-    full = max(r for r in rows2) - 1
-    for r in range(full):
+    assert rows2 == sorted(rows2)
+    for r in range(max(rows2)):
         assert all((2, r, s) in seen for s in range(2 * P)) and all((1, r, s) in seen for s in (0, 1))

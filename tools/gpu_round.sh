@@ -15,7 +15,7 @@ for step in "$@"; do
   echo "=== $step $(date +%T)"
   case $name in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg" \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "$arg" \
         > $O/tests_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40).txt 2>&1 || { tail -n 40 $O/tests_*.txt; exit 1; } ;;
     gputests)
       timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
