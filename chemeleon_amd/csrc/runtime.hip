@@ -464,7 +464,7 @@ static int batch_opts(const chm_batch_options* o, BatchOpts& bo) {
   if (!o) return CHM_OK;
   if (o->edge_style != CHM_EDGES_FC && o->edge_style != CHM_EDGES_KNN) return fail(CHM_E_ARG, "unknown edge_style");
   bo.knn = o->edge_style == CHM_EDGES_KNN;
-  if (o->max_neighbors) bo.max_nb = o->max_neighbors;
+  bo.max_nb = o->max_neighbors;  // <= 0: no neighbour cap (get_max_neighbors_mask, data_utils.py:341-348)
   if (o->knn_edges_per_atom) bo.per_atom = o->knn_edges_per_atom;
   if (bo.per_atom < 1 || bo.per_atom > 4096) return fail(CHM_E_ARG, "knn_edges_per_atom out of range");
   return CHM_OK;

@@ -11,9 +11,12 @@ pairs, D3PM / DDPM / VE updates, all in HIP kernels on the caller's stream.
 Noise
 -----
 * ``noise="torch"`` (default, parity mode): every random tensor is drawn
-  from the global CPU torch generator in the reference's order
-  (chemeleon.py:348-349, 400-404, 418, 435, 455) and uploaded, so a run
-  seeded like the reference reproduces the reference CPU trajectory.
+  from the global CPU torch generator in the order of the reference's CPU
+  path (chemeleon.py:348-349, 400-404, 418, 435, 455) and uploaded, so a run
+  seeded like the reference reproduces the reference CPU trajectory (the
+  parity target). The reference run on a GPU would draw rand_l / rand_x
+  (``randn_like`` of device tensors, :418, 435, 455) from the device
+  generator instead; that stream is not reproduced.
 * ``noise="philox"`` (throughput mode): noise is generated inside the step
   kernels from a counter-based Philox stream keyed by (seed, t, global
   node / graph index); results do not depend on how samples are sharded.
@@ -88,7 +91,9 @@ class Chemeleon(nn.Module):
         `batch` has atom_types [N], frac_coords [N,3], lattices [B,3,3], natoms [B], batch [N] and,
         for text-guided models, text (List[str]) (what Batch.from_data_list builds); `noise` =
         (t [B], rand_a [N,A], noise_lattice [B,3,3] (unmasked), noise_coords [N,3]) or None to draw
-        them in the reference's order (t from numpy, the rest from the CPU torch generator).
+        them in the order of the reference's CPU path (t from numpy, the rest from the CPU torch
+        generator; the reference on a GPU would take the randn_like draws of :174, 179 from the device
+        generator, which is not reproduced).
         Returns the reference's dict (loss, vb_loss_atom_types, ce_loss_atom_types, true / pred noise
         lattice (masked entries), true / pred noise coords). No autograd: the HIP decoder has no
         backward pass."""
@@ -174,7 +179,7 @@ class Chemeleon(nn.Module):
         from chemeleon_amd.text_encoder import CrystalClip, TextEncoder
         clip = None
         if kwargs.get("path_ckpt_clip"):
-            clip = CrystalClip.load_from_checkpoint(kwargs["path_ckpt_clip"], text_model_dir=tdir)
+            clip = CrystalClip.load_from_checkpoint(kwargs["path_ckpt_clip"], text_model_dir=tdir, graph=False)
         return TextEncoder(text_encoder_name=cfg["text_encoder"], text_embed_dim=cfg["text_embed_dim"],
                            max_text_len=cfg["max_text_len"], text_dim=cfg["text_dim"],
                            trainable_text_encoder=cfg["trainable_text_encoder"], pretrained_clip_model=clip,
@@ -314,7 +319,7 @@ class Chemeleon(nn.Module):
         as a HIP graph (chm_sample_step_dt reads t from device memory and
         decrements it) and replayed for every timestep. With noise="torch" the
         step reads its noise from fixed device buffers (chm_sample_step_dt_noise):
-        every step's draws come from the CPU generator in the reference's order
+        every step's draws come from the CPU generator in the order of the reference's CPU path
         (rand(N, A), randn(B, 3, 3), randn(N, 3), randn(N, 3)), into pinned host
         buffers (two, alternating, so the next draw overlaps the running step)
         and are copied in stream order before the replay.

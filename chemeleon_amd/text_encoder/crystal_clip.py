@@ -42,11 +42,14 @@ class CrystalClip(nn.Module):
             self.text_encoder = tf.BertModel.from_pretrained(d, local_files_only=True)
             e = self.text_embed_dim
             self.text_proj = nn.Sequential(nn.Linear(e, e), nn.LayerNorm(e), nn.GELU(), nn.Linear(e, self.clip_dim))
-        if graph and all(k in _config for k in GRAPH_KEYS):
+        # graph keys the config lacks (then no graph side is built; a checkpoint that carries one fails
+        # loudly in load_from_checkpoint, and get_graph_embeds says why)
+        self.missing_graph_keys = [k for k in GRAPH_KEYS + ("graph_pooling",) if k not in _config] if graph else []
+        if graph and not self.missing_graph_keys:
             from chemeleon_amd.modules.cspnet import CSPNet
             # graph encoder: a time- and text-free CSPNet (crystal_clip.py:34-52)
             self.graph_encoder = CSPNet(time_dim=0, text_dim=0, **{k: _config[k] for k in GRAPH_KEYS})
-            self.graph_pooling = _config.get("graph_pooling", "mean")
+            self.graph_pooling = _config["graph_pooling"]  # (required, as crystal_clip.py:53-58)
             if self.graph_pooling not in ("mean", "sum"):
                 raise ValueError(f"graph_pooling must be 'mean' or 'sum', got {self.graph_pooling!r}")
             g = _config["hidden_dim"]
@@ -63,6 +66,9 @@ class CrystalClip(nn.Module):
         crystal (scatter_mean / scatter_sum over `batch.batch`), projected. `batch` needs
         atom_types [N], frac_coords [N,3], lattices [B,3,3], natoms [B] and batch [N] (what
         Batch.from_data_list builds)."""
+        if not hasattr(self, "graph_encoder"):
+            raise RuntimeError("this CrystalClip has no graph encoder: its config lacks "
+                               f"{self.missing_graph_keys or 'nothing (built with graph=False)'}")
         out = self.graph_encoder(t=None, atom_types=batch.atom_types, frac_coords=batch.frac_coords,
                                  lattices=batch.lattices, num_atoms=batch.natoms, node2graph=batch.batch)
         h = out.node_features
@@ -81,10 +87,17 @@ class CrystalClip(nn.Module):
         return self.text_proj(out.last_hidden_state[:, 0, :])
 
     @classmethod
-    def load_from_checkpoint(cls, path: str, text_model_dir: Optional[str] = None, map_location="cpu"):
+    def load_from_checkpoint(cls, path: str, text_model_dir: Optional[str] = None, map_location="cpu",
+                             graph: bool = True):
+        """graph=False: the text side only (the sampler's conditioning front-end); the checkpoint's
+        graph_encoder.* / graph_proj.* tensors are then listed in `ignored_keys`. graph=True: a
+        checkpoint with a graph side must carry the hyper_parameters to build it."""
         ck = torch.load(path, map_location=map_location, weights_only=True)
-        m = cls(dict(ck.get("hyper_parameters", {})), text_model_dir=text_model_dir)
+        m = cls(dict(ck.get("hyper_parameters", {})), text_model_dir=text_model_dir, graph=graph)
         sd = ck["state_dict"]
+        if graph and m.missing_graph_keys and any(k.startswith(("graph_encoder.", "graph_proj.")) for k in sd):
+            raise RuntimeError("the checkpoint carries a graph encoder (graph_encoder.* / graph_proj.*) but its "
+                               f"hyper_parameters lack {m.missing_graph_keys}: cannot build it")
         own = set(m.state_dict())
         keep = {k: v for k, v in sd.items() if k in own}
         m.ignored_keys = sorted(k for k in sd if k not in keep)

@@ -141,7 +141,9 @@ int chm_batch_create_with_workspace(const chm_model* m, const int32_t* h_natoms,
 #define CHM_EDGES_KNN 1
 typedef struct chm_batch_options {
   int32_t edge_style;          /* CHM_EDGES_FC (default) or CHM_EDGES_KNN */
-  int32_t max_neighbors;       /* knn: max_num_neighbors_threshold (CSPNet max_neighbors, default 20) */
+  int32_t max_neighbors;       /* knn: max_num_neighbors_threshold (CSPNet max_neighbors, 20 in the shipped
+                                  config); <= 0 keeps every pair within the radius, as the reference's
+                                  get_max_neighbors_mask (data_utils.py:341-348) */
   int32_t knn_edges_per_atom;  /* knn: edge capacity per atom after symmetrisation (default 128); a
                                   decoder call whose graph has more edges fails with CHM_E_UNSUPPORTED */
   int32_t reserved;

@@ -96,7 +96,10 @@ def max_neighbors_mask(natoms: torch.Tensor, index: torch.Tensor, d2: torch.Tens
     max_nb = int(nnb.max()) if len(nnb) else 0
     indptr = torch.zeros(len(natoms) + 1, dtype=torch.long)
     indptr[1:] = torch.cumsum(natoms, 0)
-    per_image = segment_csr(nnb.clamp(max=thr), indptr)
+    # (thr <= 0: the reference clamps the per-image counts to 0 as well, data_utils.py:333-337, and its
+    # symmetric reorder then fails with an IndexError (cspnet.py:289-293); the uncapped graph is defined
+    # here with the true counts, so this case is parity-unpinned)
+    per_image = segment_csr(nnb.clamp(max=thr) if thr > 0 else nnb, indptr)
     if max_nb <= thr or thr <= 0:
         return torch.ones(len(index), dtype=torch.bool), per_image
     dsort = torch.full([num_atoms * max_nb], float("inf"))

@@ -105,6 +105,33 @@ def test_knn_edges_random_batches_match_oracle(model):
     assert checked == 12
 
 
+def test_knn_without_neighbour_cap_matches_oracle(g):
+    """max_neighbors <= 0 keeps every pair within the radius, the intent of the reference's
+    get_max_neighbors_mask (data_utils.py:341-348) for max_num_neighbors_threshold <= 0 (the C ABI used
+    to read 0 as 'unset' and cap at 20). Parity-unpinned: the reference also clamps its per-image
+    counts to 0 there and its symmetric reorder then raises IndexError (cspnet.py:289-293); the oracle
+    defines the uncapped graph with the true counts. On the reference's 'small' case (cells of 1-12
+    atoms, where the cap of 20 removes pairs) the device graph equals that one and is larger than the
+    capped graph."""
+    from chemeleon_amd import Chemeleon
+    cfg = default_config()
+    cfg["edge_style"] = "knn"
+    cfg["max_neighbors"] = 0
+    torch.manual_seed(0)
+    m = Chemeleon(cfg)
+    m.decoder.load_state_dict(synthetic_state_dict(default_config()))
+    m = m.to(DEV).eval()
+    assert m.decoder.max_neighbors == 0
+    nat, _, x, lat = _case(g, "small")
+    src, dst, fd = _device_edges(m, nat, x, lat)
+    ref, rfd = K.knn_edges(nat.tolist(), x, lat, 0)
+    rs, rd, rf = _grouped(ref, rfd)
+    assert len(src) == len(rs) and torch.equal(src, rs) and torch.equal(dst, rd) and torch.equal(fd, rf)
+    assert len(src) > len(g["small_edges"][0]), "the uncapped graph should be larger than the capped one"
+    del m
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("tag", ["small", "dense"])
 def test_knn_decoder_matches_reference(model, g, tag):
     sd = model.decoder.state_dict()

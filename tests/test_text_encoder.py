@@ -85,7 +85,7 @@ def test_crystal_clip_checkpoint_roundtrip(gold, tmp_path):
     hp = {"clip_dim": 32, "text_encoder": BERT_DIR, "max_text_len": 12, "text_embed_dim": 32}
     path = tmp_path / "clip.ckpt"
     torch.save({"hyper_parameters": hp, "state_dict": sd}, path)
-    c2 = CrystalClip.load_from_checkpoint(str(path), text_model_dir=BERT_DIR)
+    c2 = CrystalClip.load_from_checkpoint(str(path), text_model_dir=BERT_DIR, graph=False)  # (text side only)
     assert c2.ignored_keys == ["graph_proj.0.weight"]
     texts = [str(t) for t in gold["texts"]]
     with torch.no_grad():
@@ -116,3 +116,24 @@ def test_hub_names_need_a_local_copy(monkeypatch):
         TextEncoder("chemeleon/clip-mp-prompt")
     with pytest.raises(ValueError, match="Invalid model name"):
         TextEncoder("not-a-model")
+
+
+def test_clip_checkpoint_with_graph_side_but_no_graph_config_fails_loudly(tmp_path):
+    """A CrystalClip checkpoint whose state_dict carries graph_encoder.* / graph_proj.* tensors but whose
+    hyper_parameters lack the graph keys cannot build its graph side: loading raises and names the
+    missing keys (it used to file those tensors under ignored_keys and fail later in get_graph_embeds)."""
+    from chemeleon_amd.text_encoder import CrystalClip
+    hp = {"clip_dim": 32, "text_encoder": BERT_DIR, "max_text_len": 12, "text_embed_dim": 32}
+    clip = CrystalClip(hp, text_model_dir=BERT_DIR)
+    assert "graph_pooling" in clip.missing_graph_keys and "hidden_dim" in clip.missing_graph_keys
+    with pytest.raises(RuntimeError, match="no graph encoder"):
+        clip.get_graph_embeds(None)
+    sd = dict(clip.state_dict())
+    sd["graph_proj.0.weight"] = torch.zeros(4, 4)
+    path = tmp_path / "clip.ckpt"
+    torch.save({"state_dict": sd, "hyper_parameters": hp}, path)
+    with pytest.raises(RuntimeError, match="graph_pooling"):
+        CrystalClip.load_from_checkpoint(str(path), text_model_dir=BERT_DIR)
+    del sd["graph_proj.0.weight"]  # without graph tensors the text-only checkpoint loads
+    torch.save({"state_dict": sd, "hyper_parameters": hp}, path)
+    CrystalClip.load_from_checkpoint(str(path), text_model_dir=BERT_DIR)
