@@ -98,7 +98,8 @@ struct EdgeArgs {
             // (tests, exact results) = k_edge16_layer's layer-2 tiles always request the repair launches;
             // bit 13 (tests, exact results) = k_edge16_tail's layer-1 tiles start ~10 ms late and its
             // segment tiles wait ~2^10 spins only (a real timeout: they read S before it is written);
-            // bit 14 (tests, WRONG results) = no repair launches behind k_edge16_tail
+            // bit 14 (profiling / tests, WRONG results after a failed check) = no repair launches behind
+            // k_edge16_tail or k_edge16_layer
 };
 // Device event counters of the edge kernels (edge16.hip), cumulative over launches and graph replays
 // until chm_prof_events_reset: wait timeouts and repair launches that ran (each must read 0 in a

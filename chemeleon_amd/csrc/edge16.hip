@@ -1086,7 +1086,7 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
     hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
   }
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || (g1.dbg & 16384)) return e;  // (dbg 16384: profiling / tests, no repair launches)
   // the repair pair (exits at once unless a layer-2 tile flagged another XCD's layer-1 tile)
   EdgeArgs r1 = g1, r2 = g2;
   r1.lflags = r2.lflags = nullptr;

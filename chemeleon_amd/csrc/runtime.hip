@@ -80,6 +80,7 @@ struct chm_model {
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int ncu = 0;           // compute units of the device the model lives on
+  int repair_grid = 0;   // CHM_REPAIR_GRID: blocks of the edge kernels' repair launches (default: ncu)
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
   int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2 (two-launch schedule), 3 (k_edge16_layer)
@@ -294,6 +295,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (lay) m->edge_layer = atoi(lay);
     const char* lag = getenv("CHM_EDGE_LAG");
     if (lag) m->edge_lag = atoi(lag) > 0 ? atoi(lag) : 1;
+    const char* rg = getenv("CHM_REPAIR_GRID");
+    if (rg) m->repair_grid = atoi(rg);
     const char* dyn = getenv("CHM_EDGE_DYN");
     if (dyn) m->edge_dyn = atoi(dyn);
     const char* pool = getenv("CHM_EDGE_POOL");
@@ -1135,9 +1138,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
           e2.trace = e1.trace;
           const hipError_t r =
               m->ncu > 0 && (m->edge_dyn == 2 || (m->edge_dyn == 1 && b->nrt >= kDynMinTiles))
-                  ? edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s, b->sched + (size_t)l * (16 + 8 * b->sched_cap),
-                                      (int)b->sched_cap, m->ncu, m->edge_pool)
-                  : edge_gemm16_layer(e1, e2, m->edge_lag, m->ncu, s);
+                  ? edge_gemm16_layer(e1, e2, m->edge_lag, m->repair_grid, s,
+                                      b->sched + (size_t)l * (16 + 8 * b->sched_cap), (int)b->sched_cap, m->ncu,
+                                      m->edge_pool)
+                  : edge_gemm16_layer(e1, e2, m->edge_lag, m->repair_grid, s);
           e2.trace = nullptr;
           return r;
         }));
@@ -1155,7 +1159,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e1b.flag_row0 = e2.flag_row0 = b->l1_rows_a;
         e2.xbad = b->xbad + 32 + l;  // (a timed-out wait: the repair launches recompute edge layer 2)
         HIPCHK(edge_gemm16(e1, EPI_EDGE, s));
-        HIPCHK(edge_gemm16_tail(e1b, e2, m->ncu, s));
+        HIPCHK(edge_gemm16_tail(e1b, e2, m->repair_grid, s));
       } else {
         {
           ProfScope ps(CHM_K_EDGE_FOURIER, s);
