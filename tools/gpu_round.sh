@@ -1,6 +1,5 @@
 # One GPU-box session of checks, run from the repo root: bash tools/gpu_round.sh <tag> <steps...>
-# steps: tests=<pytest -k expr> | gputests (the whole -m gpu suite) | bench[:args] | dist2 | prof[:args] |
-#        pmc | api
+# steps: tests=<pytest -k expr> | gputests (the whole -m gpu suite) | smoke | bench[:args] | dist2 | prof[:args]
 # Every step runs under its own time limit; the first failure ends the session (no GPU step after a
 # fault, abort or timeout). Outputs go to gpurun_out/<tag>/.
 set -o pipefail
@@ -25,6 +24,9 @@ for step in "$@"; do
       f=$O/bench_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60).json
       timeout -k 10 600 python -u bench.py $arg > $f 2> $f.err || { tail -n 30 $f.err; exit 1; }
       python tools/bench_summary.py $f ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -n 20 $O/smoke.txt; exit 1; }
+      tail -n 1 $O/smoke.txt ;;
     dist2)
       f=$O/dist2.json
       CHM_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --n-samples 64 --steps 2 --warmup 1 \
