@@ -347,190 +347,9 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   }
 }
 
-// S16 node GEMM with 32-deep K-tiles (two 16-deep MFMA k-steps per barrier; k_node_gemm has one):
-// NMT x 128 tiles, 4 waves of (NMT / 2) x 64, NB blocks per CU, NST32 stages. For small grids, where the
-// K loop is bound by the per-step chain (barrier, fragment reads, A split, MFMAs) of ~1 wave per SIMD
-// rather than by the matrix pipe (M = 5120: 0.44 us per 16-deep step against 0.1 us of MFMA). Same
-// products in the same order per output as k_node_gemm: bit-identical.
-// LDS image per stage: A [NMT rows][8 pieces of 4 fp32], W [128 rows][8 pieces: hi0 hi0 lo0 lo0 hi1 hi1
-// lo1 lo1] (the split_rows_h rows of two 16-column chunks), piece p of row r at p ^ ((r >> 1) & 7): the
-// ds_read_b128 lane groups of a 32-row fragment read then cover all 64 banks.
-constexpr int NK2 = 32, ROW2 = NK2 * 4;  // 128 B rows (A fp32, W hi/lo fp16)
-template <int NMT> constexpr int STB32 = (NMT + NN) * ROW2;
-template <int NMT, int NB> constexpr int NST32 = (160 * 1024) / (NB * STB32<NMT>) < 4 ? (160 * 1024) / (NB * STB32<NMT>) : 4;
-template <int NMT, int NB>
-__global__ __launch_bounds__(256, NB) void k_node_gemm32(GemmArgs g) {
-  constexpr int NM = NMT, NI = NMT / 64, NST_ = NST32<NMT, NB>, STB_ = STB32<NMT>;
-  static_assert(NST_ >= 3, "the K loop needs 3 stages");
-  constexpr int GLA = NM / 32, GLW = 4, GL = GLA + GLW;  // glds per thread and K-tile
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int ntn = g.N / NN;
-  const long bid = g.linear_order ? (long)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(bid % ntn) * NN;
-  const long row0 = (bid / ntn) * NM;
-  const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
-  const int nk = g.K / NK2;
-  // glds: instruction q covers rows 8q + (L >> 3), LDS piece L & 7 (lane-linear) holding logical piece
-  // (L & 7) ^ swz(row); A: wave w issues q = GLA w .. GLA w + GLA-1, W: q = 4w .. 4w + 3
-  const int lr = lane >> 3, lp = lane & 7;
-  const float* asrc[GLA];
-  const float* asrc2[GLA];
-#pragma unroll
-  for (int u = 0; u < GLA; ++u) {
-    const int r = 8 * (GLA * wave + u) + lr;
-    const long ar = row0 + (r < nrows ? r : nrows - 1);
-    const int lg = lp ^ ((r >> 1) & 7);
-    asrc[u] = g.A + ar * g.lda + 4 * lg;
-    asrc2[u] = g.A2 + ar * g.lda2 + 4 * lg - g.ksplit;
-  }
-  const _Float16* Wp = reinterpret_cast<const _Float16*>(g.Wp3);
-  const _Float16* wsrc[GLW];
-#pragma unroll
-  for (int u = 0; u < GLW; ++u) {
-    const int r = 8 * (GLW * wave + u) + lr;
-    wsrc[u] = Wp + (long)(n0 + r) * 2 * g.K + 8 * (lp ^ ((r >> 1) & 7));
-  }
-  auto issue = [&](int t) {
-    const int k0 = (t < nk ? t : nk - 1) * NK2;  // past the end: re-read the last tile into an idle stage
-    char* st = lds + (t % NST_) * STB_;
-#pragma unroll
-    for (int u = 0; u < GLA; ++u) {
-      const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 8 * (GLA * wave + u) * ROW2), 16, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < GLW; ++u)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + 2 * k0), (lds_void*)(st + NM * ROW2 + 8 * (GLW * wave + u) * ROW2),
-                                       16, 0, 0);
-  };
-
-  f32x16 acc[NI][2];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  float asc[NI], aun[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) asc[i] = aun[i] = 1.0f;
-  if (g.amax) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int lrow = wm * (NM / 2) + 32 * i + r32;
-      const long ar = row0 + (lrow < nrows ? lrow : nrows - 1);
-      float m = g.amax[ar];
-      if (g.amax2) m = fmaxf(m, g.amax2[ar]);
-      int e = 0;
-      if (m > 0.f) frexpf(m, &e);
-      asc[i] = ldexpf(1.0f, -e);
-      aun[i] = ldexpf(1.0f, e);
-    }
-  }
-  // fragment rows: A wm * NM/2 + 32 i + r32, W wn * 64 + 32 j + r32 (swz depends on r32 only)
-  const int sw = (r32 >> 1) & 7;
-  const int fa = (wm * (NM / 2) + r32) * ROW2, fw = NM * ROW2 + (wn * 64 + r32) * ROW2;
-  f32x4 ra[2][NI][2];        // [k-step][i][piece pair]
-  f16x8 fa_[2][2][NI];       // [k-step][hi / lo][i]
-  f16x8 fwt[2][2][2];        // [k-step][hi / lo][j]
-  auto read = [&](int t, int ks) {
-    const char* st = lds + (t % NST_) * STB_;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      ra[ks][i][0] = *reinterpret_cast<const f32x4*>(st + fa + i * 32 * ROW2 + 16 * ((4 * ks + 2 * h) ^ sw));
-      ra[ks][i][1] = *reinterpret_cast<const f32x4*>(st + fa + i * 32 * ROW2 + 16 * ((4 * ks + 2 * h + 1) ^ sw));
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      fwt[ks][0][j] = *reinterpret_cast<const f16x8*>(st + fw + j * 32 * ROW2 + 16 * ((4 * ks + h) ^ sw));
-      fwt[ks][1][j] = *reinterpret_cast<const f16x8*>(st + fw + j * 32 * ROW2 + 16 * ((4 * ks + 2 + h) ^ sw));
-    }
-  };
-  auto split = [&](int ks) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const f32x2 x = (e < 4 ? f32x2{ra[ks][i][0][e], ra[ks][i][0][e + 1]} : f32x2{ra[ks][i][1][e - 4], ra[ks][i][1][e - 3]}) * asc[i];
-        const f16x2 hi = __builtin_convertvector(x, f16x2);
-        const f16x2 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
-        fa_[ks][0][i][e] = hi[0]; fa_[ks][0][i][e + 1] = hi[1];
-        fa_[ks][1][i][e] = lo[0]; fa_[ks][1][i][e + 1] = lo[1];
-      }
-  };
-  // small terms first (a_lo w_hi, a_hi w_lo), the leading product last: as k_node_gemm's S16 order
-  auto mfmas = [&](int ks) {
-    constexpr int PA[3] = {1, 0, 0}, PW[3] = {0, 1, 0};
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fwt[ks][PW[k]][j], fa_[ks][PA[k]][i], acc[i][j], 0, 0, 0);
-  };
-#pragma unroll
-  for (int t = 0; t < NST_ - 1; ++t) issue(t);
-  for (int t = 0; t < nk; ++t) {
-    // tile t has landed for this thread (tiles t+1 .. t+NST-2 may stay in flight), then for everyone;
-    // after the barrier tile t-1's stage (read in step t-1) takes tile t+NST-1
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST_ - 2) * GL) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(t + NST_ - 1);
-    read(t, 0);
-    read(t, 1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_setprio(1);
-    split(0);
-    mfmas(0);
-    split(1);  // (its VALU issues beside k-step 0's MFMAs)
-    mfmas(1);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the block exits
-
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const long lrow = wm * (NM / 2) + i * 32 + r32;
-    float cm = 0.f;
-    if (lrow < nrows) {
-      const long row = row0 + lrow;
-      const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
-          f32x4 v;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-          v *= *reinterpret_cast<const f32x4*>(g.wscale + col) * aun[i];
-          if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
-          if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
-          if (g.act == 1)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
-          if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
-          *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
-          cm = fmaxf(cm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-        }
-    }
-    if (g.cmax) {
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      if (h == 0 && lrow < nrows) atomicMax(g.cmax + row0 + lrow, __float_as_uint(cm));
-    }
-  }
-}
-
 int g_node_variant = 0;
-int g_node_k32 = -1;  // 32-deep K-tiles for small grids: -1 = default (CHM_NODE_K32, on), 0 off, 1 on
 
 constexpr int LDS3 = STB<true> * NST<true, 3>;
-constexpr int LDS32_64 = STB32<64> * NST32<64, 2>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
 
 hipError_t node_gemm_init() {
@@ -542,8 +361,6 @@ hipError_t node_gemm_init() {
   const int bytes[10] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4};
   hipError_t e = hipSuccess;
   for (int i = 0; i < 10 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_node_gemm32<64, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS32_64);
   return e;
 }
 
@@ -571,13 +388,8 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   // 26 us at K = 512); above that 128-row tiles at three blocks per CU (M = 20480: 54 vs 65 us with
   // two), profiles/r2/node/node64_micro.log
   const int rows = g_node_rows ? g_node_rows : (blocks < 256 ? 64 : 128);
-  if (g_node_k32 < 0) g_node_k32 = getenv("CHM_NODE_K32") ? atoi(getenv("CHM_NODE_K32")) : 1;
   if (g.wscale && rows == 64) {
     const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
-    if (g_node_k32 && !v1 && g.K % NK2 == 0 && g.ksplit % NK2 == 0 && !g_node_blocks) {
-      hipLaunchKernelGGL((k_node_gemm32<64, 2>), grid64, block, LDS32_64, s, g);
-      return hipGetLastError();
-    }
     if (g_node_blocks == 4)
       hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 4, 64> : k_node_gemm<0, true, 4, 64>), grid64, block, LDS64_4, s, g);
     else

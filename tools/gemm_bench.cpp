@@ -128,39 +128,6 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  if (argc > 3 && std::string(argv[3]) == "node32") {  // 64-row S16 node GEMM: 16- vs 32-deep K-tiles
-    CK(node_gemm_init());
-    void* W16; float* wsc16; float* amax; float* C2;
-    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
-    CK(hipMalloc(&C2, M * N * 4));
-    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
-    std::vector<float> one(M, 1.0f);
-    CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
-    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax;
-    g_node_rows = 64;
-    for (int rep = 0; rep < 3; ++rep) {
-      g_node_k32 = 0;
-      const float t16 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
-      g_node_k32 = 1;
-      const float t32 = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
-      printf("M=%ld N=%d K=%d 64-row tiles: 16-deep %.2f us, 32-deep %.2f us (%.1f TF fp32-eq)\n", M, N, K, t16 * 1e3,
-             t32 * 1e3, flops / t32 / 1e9);
-    }
-    const size_t nc = (size_t)M * N;
-    std::vector<float> a(nc), b(nc);
-    g_node_k32 = 0;
-    CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(a.data(), C, nc * 4, hipMemcpyDeviceToHost));
-    g_node_k32 = 1;
-    GemmArgs g2 = g16; g2.C = C2;
-    CK(node_gemm(g2, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(b.data(), C2, nc * 4, hipMemcpyDeviceToHost));
-    size_t diff = 0;
-    for (size_t i = 0; i < nc; ++i) diff += a[i] != b[i];
-    printf("  bit-identical: %s (%zu of %zu differ)\n", diff ? "NO" : "yes", diff, nc);
-    g_node_rows = 0; g_node_k32 = -1;
-    return 0;
-  }
   if (argc > 3 && std::string(argv[3]) == "nodefix") {  // split16 node GEMM time vs K (fixed cost = intercept)
     CK(node_gemm_init());
     void* W16; float* wsc16; float* amax;
