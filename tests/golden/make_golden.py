@@ -298,12 +298,15 @@ def large_step_natoms(tag):
         return [40] * 256
     if tag == "64x40":
         return [40] * 64
+    if tag == "512x40":  # configs[3] as one batch (the 1-GPU bench workload)
+        return [40] * 512
     if tag == "c4chunk256":  # configs[4]: natoms = randint(1, 81, generator seed 7), first 256
         return torch.randint(1, 81, (2048,), generator=torch.Generator().manual_seed(7))[:256].tolist()
     raise KeyError(tag)
 
 
-LARGE_STEPS = (("256x40", [1000, 500, 2, 1]), ("64x40", [1000, 500, 1]), ("c4chunk256", [1000, 500, 2, 1]))
+LARGE_STEPS = (("256x40", [1000, 500, 2, 1]), ("64x40", [1000, 500, 1]), ("c4chunk256", [1000, 500, 2, 1]),
+               ("512x40", [1000, 500, 1]))
 
 
 def gen_large_steps(chm, csp):
@@ -311,7 +314,10 @@ def gen_large_steps(chm, csp):
     are stored; the noise is regenerated from its seed (torch CPU generator) by the test."""
     T = 1000
     m, sd = build_reference_model(chm, csp, T)
+    only = os.environ.get("CHM_GOLDEN_TAGS")  # (regenerate a subset: comma-separated tags)
     for tag, ts in LARGE_STEPS:
+        if only and tag not in only.split(","):
+            continue
         natoms = large_step_natoms(tag)
         B, N = len(natoms), sum(natoms)
         rec = {"natoms": torch.tensor(natoms), "ts": np.array(ts), "weights_crc": weights_crc(sd)}
