@@ -205,11 +205,12 @@ def test_teacher_forced_steps(model1000, golden, cn, tag, math):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("tag", ["256x40", "64x40", "c4chunk256"])
+@pytest.mark.parametrize("tag", ["256x40", "64x40", "c4chunk256", "512x40"])
 def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
     """BASELINE sizes, one full reverse step each against the reference (fixtures written by the
     reference itself, tests/golden/make_golden.py steps_large): configs[2] (256 x 40), the per-GPU
-    shard of configs[3] (64 x 40) and the first 256 crystals of configs[4]
+    shard of configs[3] (64 x 40), configs[3] whole as one batch (512 x 40, the 1-GPU bench
+    workload) and the first 256 crystals of configs[4]
     (natoms = randint(1, 81, seed 7)), which puts crystals of 1 to 80 atoms, segment tiles that
     span several small crystals and the gather path of the edge epilogues through the whole step.
     Same gates as test_teacher_forced_steps: types bit-exact, |dx| <= 1e-4 periodic, lattices 1e-4."""
