@@ -14,6 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libchemeleon_hip.so")
+# (A/B builds only: extra -D flags and another output path, e.g. CHM_BUILD_DEFS="-DCHM_X=1"
+# CHM_BUILD_LIB=abl/x/libchemeleon_hip.so, loaded with CHM_LIB; the product build sets neither)
+DEFS = os.environ.get("CHM_BUILD_DEFS", "").split()
+if os.environ.get("CHM_BUILD_LIB"):
+    LIB = os.path.abspath(os.environ["CHM_BUILD_LIB"])
+    LIBDIR = os.path.dirname(LIB)
 SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "split16.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip"]
 ARCH = os.environ.get("CHM_OFFLOAD_ARCH", "gfx950")
 
@@ -41,7 +47,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     def compile_one(src):
         obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src),
-               "-o", obj, "-Wno-unused-result"]
+               "-o", obj, "-Wno-unused-result"] + DEFS
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
