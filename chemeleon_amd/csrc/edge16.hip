@@ -27,13 +27,6 @@ namespace chm {
 
 #include "edge_common.h"
 
-// Edge layer 1's S stores: half lines (each lane its own row's pieces) or whole lines (a DPP exchange
-// between the lanes of rows 2p, 2p+1). Same bytes at the same addresses; A/B builds set it.
-#ifndef CHM_S_HALF_LINES
-#define CHM_S_HALF_LINES 0
-#endif
-constexpr bool kHalfLines = CHM_S_HALF_LINES;
-
 namespace {
 
 __device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
@@ -548,37 +541,6 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         const int ex2 = exp_of(mx);
         const float sc = ldexpf(1.0f, -ex2);
         const long orow = (long)c * g.E + rowv[i];
-        if constexpr (kHalfLines) {
-          // Half-line stores: a lane writes its own row's hi piece (16 B of the line's hi half) and lo
-          // piece; the row's four lanes cover its line, 16 half lines per instruction, no lane exchange.
-          _Float16* sr = S0 + orow * (2 * H) + ((n0 + wn * 128) / 32) * 64 + 8 * g4;
-          const bool st = lr < nrows && !nostore;
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            f16x8 hv, lv;
-#pragma unroll
-            for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-              for (int r = 0; r < 4; r += 2) {
-                const float v0 = v[2 * cc + a2][r], v1 = v[2 * cc + a2][r + 1];
-                const f16x2 h2 = __builtin_convertvector(f32x2e{v0, v1} * sc, f16x2);
-                const f16x2 l2 = lo_pair(v0, v1, sc, h2);
-                hv[4 * a2 + r] = h2.x;
-                hv[4 * a2 + r + 1] = h2.y;
-                lv[4 * a2 + r] = l2.x;
-                lv[4 * a2 + r + 1] = l2.y;
-              }
-            if (st) {
-              *reinterpret_cast<f16x8*>(sr + cc * 64) = hv;
-              *reinterpret_cast<f16x8*>(sr + cc * 64 + 32) = lv;
-            }
-          }
-          if (lr < nrows && !nostore && g4 == 0) {
-            signed char* pe = reinterpret_cast<signed char*>(g.sexp) + orow * 4 + (n0 + wn * 128) / CHUNK;
-            *pe = (signed char)ex2;
-          }
-          return;
-        }
         // Whole-line stores: a row's 32-column chunk is one 128-B line [hi 32 | lo 32], held by the
         // row's four lanes (16 B of hi and 16 B of lo each). Lanes l16 and l16 ^ 1 (rows 2p, 2p+1)
         // swap a piece (DPP), so that one store writes row 2p's whole line (even lanes its hi half,

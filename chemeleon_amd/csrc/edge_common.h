@@ -6,7 +6,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
@@ -43,17 +42,6 @@ __device__ __forceinline__ f32x2e silu_e2(f32x2e x) {
   t.x = __builtin_amdgcn_rcpf(t.x);
   t.y = __builtin_amdgcn_rcpf(t.y);
   return x * t;
-}
-
-// The lo halves of a split pair: fp16(v_k s - h_k) for k = 0, 1, s a power of two, h = fp16(v s): one
-// v_fma_mix per element (exact product, one rounding), where the compiler would convert h back to
-// fp32 and run a packed fma plus a packed conversion (2 instructions per element instead of 1).
-// VALU only; bit-identical to (_Float16)(v * s - (float)h).
-__device__ __forceinline__ f16x2 lo_pair(float v0, float v1, float s, f16x2 h) {
-  f16x2 l;
-  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(v0), "v"(s), "v"(h));
-  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(v1), "v"(s), "v"(h));
-  return l;
 }
 
 __device__ __forceinline__ long remap(long b, long nb) {

@@ -46,17 +46,15 @@ constexpr int A_ROWB = NK * 4, W_ROWB = NK * 2;  // 64 B, 32 B
 constexpr int W_PLB = NN * W_ROWB;               // 4 KB per plane
 template <int NMT> constexpr int A_STB = NMT * A_ROWB;  // 8 KB (128 rows), 4 KB (64 rows)
 // bf16x3: A + three W planes (20 KB) x 4 stages; S16: A + W hi/lo rows (8 + 8 KB) x 5 stages
-template <bool S16, int NMT = 128, int NNT = 128>
-constexpr int STB = S16 ? A_STB<NMT> + 2 * W_PLB * (NNT / NN) : A_STB<NMT> + 3 * W_PLB;
+template <bool S16, int NMT = 128> constexpr int STB = S16 ? A_STB<NMT> + 2 * W_PLB : A_STB<NMT> + 3 * W_PLB;
 // NB = blocks per CU. 128-row tiles: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of
 // 16 KB); 64-row tiles (S16): 3 (4 stages of 12 KB) or 4 (3 stages)
-template <bool S16, int NB, int NMT = 128, int NNT = 128>
-constexpr int NST = NNT == 256 ? 4 : NMT == 64 ? (NB == 3 ? 4 : 3) : NB == 3 ? 3 : (S16 ? 5 : 4);
+template <bool S16, int NB, int NMT = 128>
+constexpr int NST = NMT == 64 ? (NB == 3 ? 4 : 3) : NB == 3 ? 3 : (S16 ? 5 : 4);
 constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
 static_assert(STB<true> * NST<true, 2> <= NODE_LDS && STB<false> * NST<false, 2> <= NODE_LDS, "LDS");
 static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
 static_assert(3 * STB<true, 64> * NST<true, 3, 64> <= 160 * 1024 && 4 * STB<true, 64> * NST<true, 4, 64> <= 160 * 1024, "LDS");
-static_assert(STB<true, 128, 256> * NST<true, 1, 128, 256> <= 160 * 1024, "LDS");
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -81,32 +79,25 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 }  // namespace
 
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR, bool S16, int NB, int NMT = 128, int NNT = 128>
-__global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k_node_gemm(GemmArgs g) {
-  static_assert(NNT == 256 ? S16 && NMT == 128 && NB == 1
-                           : NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4),
-                "tiling");
-  // 128x128 / 64x128 tiles: 4 waves of (NM/2) x 64; 128x256 tiles: 8 waves of 32 x 128
-  constexpr int NWAVES = NNT == 256 ? 8 : 4, WROWS = NNT == 256 ? NMT / 4 : NMT / 2;
-  constexpr int NM = NMT, NI = WROWS / 32;  // tile rows; 32-row fragment groups per wave
-  constexpr int NJ = NNT / 64;              // 32-column fragment groups per wave (wave tile WROWS x NNT/2)
-  constexpr int AGI = NM / 16 / NWAVES;     // A glds per thread and K-tile (16 rows each)
+template <int VAR, bool S16, int NB, int NMT = 128>
+__global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
+  static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4), "tiling");
+  constexpr int NM = NMT, NI = NMT / 64;  // tile rows; 32-row fragment groups per wave
   constexpr int A_STB_ = A_STB<NMT>;
   // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
   // step t's barrier it takes tile t + NST while tiles t+1 .. t+NST-1 are in flight or landed.
-  constexpr int STB_ = STB<S16, NMT, NNT>, NST_ = NST<S16, NB, NMT, NNT>, AHEAD = NST_;
-  constexpr int NWI = S16 ? NNT / 16 / NWAVES : 3;                       // W glds per thread and K-tile
-  constexpr int GL = S16 ? NWI + AGI : 5;                                // glds per thread and K-tile
+  constexpr int STB_ = STB<S16, NMT>, NST_ = NST<S16, NB, NMT>, AHEAD = NST_;
+  constexpr int GL = S16 ? 2 + NI : 5;                                   // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
-  const int ntn = g.N / NNT;
+  const int ntn = g.N / NN;
   // XCD-aware order (workgroups go round-robin to the 8 XCDs): each XCD takes a contiguous range of
   // tiles, so the column tiles of a row tile run on one XCD and read their A rows once from HBM
   // (without it every column tile fetched A again into another XCD's L2: 538 MB per launch vs 84-168)
   const long bid = g.linear_order ? (long)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(bid % ntn) * NNT;
+  const int n0 = (int)(bid % ntn) * NN;
   const long row0 = (bid / ntn) * NM;
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
   const int nk = g.K / NK;
@@ -116,19 +107,20 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
   // W: instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1 holding
   // logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
   const int alp = (lane & 3) ^ ((lane >> 4) & 3);
-  const float* asrc[AGI];
-  const float* asrc2[AGI];
+  const float* asrc[NI];
+  const float* asrc2[NI];
 #pragma unroll
-  for (int u = 0; u < AGI; ++u) {
-    const int r = 16 * (AGI * wave + u) + (lane >> 2);
+  for (int u = 0; u < NI; ++u) {
+    const int r = 16 * (NI * wave + u) + (lane >> 2);
     const long ar = row0 + (r < nrows ? r : nrows - 1);
     asrc[u] = g.A + ar * g.lda + 4 * alp;
     asrc2[u] = g.A2 + ar * g.lda2 + 4 * alp - g.ksplit;
   }
   // W (bf16x3): instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1
   // holding logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
-  // W (S16): rows of 64 B [hi 16 | lo 16] per K-tile, swizzled like A; instruction q (of 4 NJ) covers
-  // rows 16q + (L >> 2), LDS piece L & 3 holding logical piece alp; wave w issues q = NJ w .. NJ w + NJ-1.
+  // W (S16): rows of 64 B [hi 16 | lo 16] per K-tile, swizzled like A; instruction q (of 8) covers
+  // rows 16q + (L >> 2), LDS piece L & 3 holding logical piece alp; wave w issues q = 2w, 2w + 1.
+  constexpr int NWI = S16 ? 2 : 3;
   const int wlp = (lane & 1) ^ ((lane >> 4) & 1);
   const __bf16* Wpl = reinterpret_cast<const __bf16*>(g.Wp3);
   const long wplane = (long)g.N * g.K;
@@ -137,7 +129,7 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
 #pragma unroll
   for (int u = 0; u < NWI; ++u) {
     if constexpr (S16) {
-      const int q = NWI * wave + u;
+      const int q = 2 * wave + u;
       wsrc[u] = Wpl + (long)(n0 + 16 * q + (lane >> 2)) * 2 * g.K + 8 * alp;
       wdst[u] = A_STB_ + q * 1024;
     } else {
@@ -150,24 +142,24 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
     const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
     char* st = lds + (t % NST_) * STB_;
 #pragma unroll
-    for (int u = 0; u < AGI; ++u) {
+    for (int u = 0; u < NI; ++u) {
       const float* src = k0 < g.ksplit ? asrc[u] + k0 : asrc2[u] + k0;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (AGI * wave + u) * A_ROWB), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(st + 16 * (NI * wave + u) * A_ROWB), 16, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < NWI; ++u)
       __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + (S16 ? 2 * k0 : k0)), (lds_void*)(st + wdst[u]), 16, 0, 0);
   };
 
-  f32x16 acc[NI][NJ];
+  f32x16 acc[NI][2];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  // fragment offsets: A row wm*NM/2 + 32i + r32 pieces 2h, 2h+1; W row wn*NNT/2 + 32j + r32 piece h
+  // fragment offsets: A row wm*NM/2 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
   const int asw = (r32 >> 2) & 3, wsw = (r32 >> 3) & 1;
   // S16: this lane's A rows (wm*NM/2 + 32i + r32) and their power-of-two scales
   float asc[NI], aun[NI];
@@ -177,7 +169,7 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
     if (g.amax) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const int lr = wm * WROWS + 32 * i + r32;
+        const int lr = wm * (NM / 2) + 32 * i + r32;
         const long ar = row0 + (lr < nrows ? lr : nrows - 1);
         float m = g.amax[ar];
         if (g.amax2) m = fmaxf(m, g.amax2[ar]);
@@ -188,11 +180,11 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
       }
     }
   }
-  const int fa0 = (wm * WROWS + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
-  const int fa1 = (wm * WROWS + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
+  const int fa0 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
+  const int fa1 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
   const int fw = A_STB_ + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
-  const int fw16[2] = {A_STB_ + (wn * (NNT / 2) + r32) * 64 + 16 * (h ^ asw),         // hi piece h
-                       A_STB_ + (wn * (NNT / 2) + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
+  const int fw16[2] = {A_STB_ + (wn * 64 + r32) * 64 + 16 * (h ^ asw),         // hi piece h
+                       A_STB_ + (wn * 64 + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
 
   // Software pipeline (VAR 0): while the 24 MFMAs of K-tile t run, the fragments of tile t+1 are
   // read from LDS and its A part is split, both interleaved between the MFMAs (the split's VALU
@@ -200,7 +192,7 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
   constexpr int NP = S16 ? 2 : 3;  // operand parts
   typedef std::conditional_t<S16, f16x8, bf16x8> frag;
   f32x4 ra0[NI], ra1[NI];
-  frag fa[2][NP][NI], fwt[2][NP][NJ];  // [set][part][i / j]
+  frag fa[2][NP][NI], fwt[2][NP][2];  // [set][part][i / j]
   auto read_raw = [&](int t, int set) {
     const char* st = lds + (t % NST_) * STB_;
 #pragma unroll
@@ -211,7 +203,7 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-      for (int j = 0; j < (S16 ? NJ : 2); ++j)
+      for (int j = 0; j < 2; ++j)
         fwt[set][p][j] = S16 ? *reinterpret_cast<const frag*>(st + fw16[p] + j * 32 * 64)
                              : *reinterpret_cast<const frag*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
   };
@@ -252,7 +244,7 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
+        for (int j = 0; j < 2; ++j) {
           if constexpr (S16)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fwt[set][PW[k]][j], fa[set][PA[k]][i], acc[i][j], 0, 0, 0);
           else
@@ -279,19 +271,19 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
     if constexpr (S16) {
-      mfmas(cur, 0, 1);                               // NI NJ MFMAs beside the 2 NJ + 2 NI fragment reads
+      mfmas(cur, 0, 1);                               // 2 NI MFMAs beside the 4 + 2 NI fragment reads
 #pragma unroll
-      for (int k = 0; k < NI * NJ; ++k) {
+      for (int k = 0; k < 2 * NI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, (2 * NI + 2 * NJ + NI * NJ - 1) / (NI * NJ), 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NI == 2 ? 2 : 3, 0);
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       split(cur ^ 1);
-      mfmas(cur, 1, 3);                               // 2 NI NJ MFMAs, the split's VALU between them
+      mfmas(cur, 1, 3);                               // 4 NI MFMAs, the split's VALU between them
 #pragma unroll
-      for (int k = 0; k < 2 * NI * NJ; ++k) {
+      for (int k = 0; k < 4 * NI; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x002, NI * NJ == 4 ? 5 : 3, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
       }
     } else {
       mfmas(cur, 0, 2);                               // 8 MFMAs beside the 10 fragment reads
@@ -322,16 +314,16 @@ __global__ __launch_bounds__(NNT == 256 ? 512 : 256, NNT == 256 ? 1 : NB) void k
   // consecutive columns wn*64 + 32j + 8q + 4h .. +3
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const long lr = wm * WROWS + i * 32 + r32;
+    const long lr = wm * (NM / 2) + i * 32 + r32;
     float cm = 0.f;  // max |C| over this lane's columns of the row
     if (lr < nrows) {
       const long row = row0 + lr;
       const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int col = n0 + wn * (NNT / 2) + j * 32 + 8 * q + 4 * h;
+          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
@@ -359,32 +351,26 @@ int g_node_variant = 0;
 
 constexpr int LDS3 = STB<true> * NST<true, 3>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
-constexpr int LDSW = STB<true, 128, 256> * NST<true, 1, 128, 256>;  // 128x256 tiles, one block of 8 waves per CU
 
 hipError_t node_gemm_init() {
-  const void* ks[12] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
+  const void* ks[10] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
                         (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
                         (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
                         (const void*)k_node_gemm<0, true, 3, 64>, (const void*)k_node_gemm<1, true, 3, 64>,
-                        (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>,
-                        (const void*)k_node_gemm<0, true, 1, 128, 256>, (const void*)k_node_gemm<1, true, 1, 128, 256>};
-  const int bytes[12] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4, LDSW, LDSW};
+                        (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>};
+  const int bytes[10] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 12 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  for (int i = 0; i < 10 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
-int g_node_wide = -1;   // S16 128x256 tiles: -1 = CHM_NODE_WIDE or by grid size (kWideMinTiles), 0 = never, 1 = whenever N allows
-constexpr long kWideMinTiles = 512;  // two rounds of 128x256 tiles
 int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
 hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   static const int linear = getenv("CHM_NODE_LINEAR") ? atoi(getenv("CHM_NODE_LINEAR")) : 0;  // (A/B only)
-  static const int wide_env = getenv("CHM_NODE_WIDE") ? atoi(getenv("CHM_NODE_WIDE")) : 0;      // (A/B only)
-  const int wide = g_node_wide >= 0 ? g_node_wide : wide_env;
   GemmArgs g = g_in;
   g.linear_order = linear;
   if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
@@ -402,15 +388,6 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   // 26 us at K = 512); above that 128-row tiles at three blocks per CU (M = 20480: 54 vs 65 us with
   // two), profiles/r2/node/node64_micro.log
   const int rows = g_node_rows ? g_node_rows : (blocks < 256 ? 64 : 128);
-  // S16, large grids: 128x256 tiles, one block of 8 waves (32x128 each) per CU: per MFMA, half the A
-  // split VALU and 3/4 of the LDS-DMA issues of the 128x128 tiling
-  const long wide_tiles = ((g.M + 127) / 128) * (g.N / 256);
-  if (g.wscale && rows == 128 && g.N % 256 == 0 && !g_node_blocks &&
-      (wide == 1 || (wide < 0 && wide_tiles >= kWideMinTiles))) {
-    hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 1, 128, 256> : k_node_gemm<0, true, 1, 128, 256>),
-                       dim3((unsigned)wide_tiles), dim3(512), LDSW, s, g);
-    return hipGetLastError();
-  }
   if (g.wscale && rows == 64) {
     const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
     if (g_node_blocks == 4)

@@ -440,11 +440,6 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_dbg = value ? (m->edge_dbg | 16384) : (m->edge_dbg & ~16384);
     return CHM_OK;
   }
-  if (k == "node_wide") {  // split16 node GEMMs on 128x256 tiles: -1 by grid size, 0 never, 1 always; bit-identical
-    if (value < -1 || value > 1) return fail(CHM_E_ARG, "node_wide must be -1, 0 or 1");
-    g_node_wide = (int)value;  // (process-wide, like the other node-GEMM tiling switches)
-    return CHM_OK;
-  }
   if (k == "edge_rows_nowait") {  // (tests) row tiles never wait for the previous tile: the msgbuf path
     m->edge_dbg = value ? (m->edge_dbg | 64) : (m->edge_dbg & ~64);
     return CHM_OK;

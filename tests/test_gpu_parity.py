@@ -351,33 +351,6 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
             assert torch.equal(u, v), f"{what}: {name} differ from node-aligned segment tiles"
 
 
-@pytest.mark.parametrize("nat", [[40] * 256, [23, 7, 40, 1, 80, 61] * 40])
-def test_node_gemm_wide_tiles_are_bit_identical(cn, nat):
-    """Split16 node GEMMs on 128x256 tiles (8 waves of 32 x 128; the default from 512 such tiles on,
-    option 'node_wide') against 128x128 tiles (4 waves of 64 x 64): same MFMA, same K order, same
-    product order per output, so one reverse step agrees bit for bit (256 x 40 and a ragged batch,
-    both above the 128-row threshold)."""
-    B, N = len(nat), sum(nat)
-    g = torch.Generator().manual_seed(31)
-    a0 = torch.randint(0, 100, (N,), generator=g)
-    x0 = torch.rand(N, 3, generator=g)
-    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
-    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
-          torch.randn(N, 3, generator=g))
-    model = _model(1000)
-    outs = []
-    try:
-        for wide in (0, 1):
-            model.decoder.set_option("node_wide", wide)
-            outs.append([o.cpu() for o in model.reverse_step(700, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
-    finally:
-        model.decoder.set_option("node_wide", -1)
-    del model
-    torch.cuda.empty_cache()
-    for u, v, what in zip(outs[0], outs[1], ("types", "frac", "lattice")):
-        assert torch.equal(u, v), f"{what}: 128x256 node-GEMM tiles differ from 128x128"
-
-
 def test_one_grid_edge_layers_single_conditioning(cn):
     """k_edge16_layer with one conditioning (P = 1: a plain decoder call, as the CrystalClip graph
     encoder and `CSPNet.forward` make): 64 x 40 (400 row tiles, above the one-grid threshold) and a
