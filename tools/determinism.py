@@ -29,6 +29,7 @@ def main():
     p.add_argument("--n-atoms", type=int, default=40)
     a = p.parse_args()
     cfg = default_config()
+    torch.manual_seed(0)  # (SigmaScheduler's sigmas_norm is a Monte-Carlo estimate drawn from the CPU generator)
     model = Chemeleon(cfg)
     model.decoder.load_state_dict(synthetic_state_dict(cfg))
     model = model.to("cuda:0").eval()
@@ -58,7 +59,8 @@ def main():
         outs.append([o.node_features.cpu().numpy(), o.atom_types_out.cpu().numpy(), o.coords_out.cpu().numpy(),
                      o.lattice_out.cpu().numpy()])
     for k, name in enumerate(("dec_h", "dec_types", "dec_coords", "dec_lattice")):
-        res[name] = outs[0][k]
+        if k:  # (node features stay out of the file: 84 MB at 512 x 40; compared in-process above)
+            res[name] = outs[0][k]
     same = [all(np.array_equal(u, v) for u, v in zip(outs[0], s)) for s in outs[1:]]
     print(f"decoder repeats bit-identical in-process: {same}")
     np.savez(a.out, **res)

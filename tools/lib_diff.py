@@ -23,6 +23,7 @@ def run(out, n_samples, n_atoms, ts):
     from chemeleon_amd.synthetic import synthetic_state_dict, synthetic_text_embeds
 
     cfg = default_config()
+    torch.manual_seed(0)  # (SigmaScheduler's sigmas_norm is a Monte-Carlo estimate drawn from the CPU generator)
     model = Chemeleon(cfg)
     model.decoder.load_state_dict(synthetic_state_dict(cfg))
     model = model.to("cuda:0").eval()
