@@ -213,7 +213,8 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
     workload) and the first 256 crystals of configs[4]
     (natoms = randint(1, 81, seed 7)), which puts crystals of 1 to 80 atoms, segment tiles that
     span several small crystals and the gather path of the edge epilogues through the whole step.
-    Same gates as test_teacher_forced_steps: types bit-exact, |dx| <= 1e-4 periodic, lattices 1e-4."""
+    Same gates as test_teacher_forced_steps: types bit-exact (at t = 1 up to 2 fp32 near-ties of the
+    logits' argmax, _t1_near_ties), |dx| <= 1e-4 periodic, lattices 1e-4."""
     g = golden(f"step_{tag}.npz")
     nat = g["natoms"].tolist()
     B, N = len(nat), sum(nat)
@@ -230,11 +231,42 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
                                            torch.from_numpy(g[f"t{t}_x"]), torch.from_numpy(g[f"t{t}_l"]), nat,
                                            2.0, 1e-5, cn[0], cn[1], noise=nz)
         ref_a = g[f"t{t}_a_out"].astype(np.int64)
-        flips = int((a.cpu().numpy() != ref_a).sum())
-        assert flips == 0, f"{tag} t={t}: {flips} of {N} atom types differ"
+        flipped = np.nonzero(a.cpu().numpy() != ref_a)[0]
+        ties = ""
+        if len(flipped):
+            assert t == 1, f"{tag} t={t}: {len(flipped)} of {N} atom types differ"
+            ties = _t1_near_ties(model1000, g, nat, cn, flipped, ref_a)
         dx = periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"{tag} frac t={t}")
         dl = close(lat.cpu(), g[f"t{t}_l_out"], what=f"{tag} lattice t={t}")
-        print(f"{tag} t={t}: types bit-exact ({N} atoms), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
+        print(f"{tag} t={t}: types bit-exact ({N} atoms{ties}), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
+
+
+def _t1_near_ties(model, g, nat, cn, flipped, ref_a):
+    """At t = 1 the types are the argmax of the CFG-mixed logits (no Gumbel noise, chemeleon.py:418 /
+    diff_utils.py:286), so two classes whose logits agree to fp32 rounding are a tie that any other
+    summation order may break the other way (512 x 40, atom 7124: top-2 gap 2.4e-6 on logits of 4.41 in
+    the reference's own arithmetic, a few ulps). Such a flip is accepted only for near-ties: at most 2
+    atoms, each with the device's own top-2 gap below 1e-5 of the atom's logit scale and the reference's
+    choice one of the two. Returns the note printed with the step."""
+    assert len(flipped) <= 2, f"t=1: {len(flipped)} atom types differ"
+    B = len(nat)
+    nat_t = torch.tensor(nat)
+    te = model.time_embed(torch.full((B,), 1, dtype=torch.long)).to(DEV)
+    kw = dict(atom_types=torch.from_numpy(g["t1_a"].astype(np.int64)).to(DEV),
+              frac_coords=torch.from_numpy(g["t1_x"]).to(DEV), lattices=torch.from_numpy(g["t1_l"]).to(DEV),
+              num_atoms=nat_t.to(DEV), node2graph=torch.arange(B).repeat_interleave(nat_t).to(DEV), t=te)
+    pc = model.decoder(text_embeds=cn[0].expand(B, -1).to(DEV), **kw).atom_types_out
+    pn = model.decoder(text_embeds=cn[1].expand(B, -1).to(DEV), **kw).atom_types_out
+    mixed = ((1 - 2.0) * pn + 2.0 * pc).cpu()
+    notes = []
+    for i in flipped.tolist():
+        top = torch.topk(mixed[i], 2)
+        gap = float(top.values[0] - top.values[1])
+        scale = float(mixed[i].abs().max())
+        assert gap <= 1e-5 * scale and int(ref_a[i]) in top.indices.tolist(), \
+            f"t=1 atom {i}: not a near-tie (top-2 gap {gap:.2e} of scale {scale:.2f}, reference class {int(ref_a[i])})"
+        notes.append(f"atom {i} gap {gap:.1e}")
+    return "; near-tie flips: " + ", ".join(notes)
 
 
 @pytest.mark.parametrize("nat", [[40] * 64, [50] * 40, [23, 7, 40, 1, 80] * 23])
