@@ -233,12 +233,20 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
         ref_a = g[f"t{t}_a_out"].astype(np.int64)
         flipped = np.nonzero(a.cpu().numpy() != ref_a)[0]
         ties = ""
+        keep = np.ones(N, dtype=bool)
         if len(flipped):
             assert t == 1, f"{tag} t={t}: {len(flipped)} of {N} atom types differ"
             ties = _t1_near_ties(model1000, g, nat, cn, flipped, ref_a)
-        dx = periodic_close(x.cpu(), g[f"t{t}_x_out"], what=f"{tag} frac t={t}")
+            # the corrector's decoder call reads the new types, so a crystal with a tie-broken type takes
+            # another coordinate step: its atoms leave the coordinate comparison (the lattice update
+            # precedes the types and stays compared for every crystal)
+            n2g = np.repeat(np.arange(B), nat)
+            keep = ~np.isin(n2g, n2g[flipped])
+            ties += f"; {int((~keep).sum())} atoms of {len(np.unique(n2g[flipped]))} crystal(s) not compared"
+        dx = periodic_close(x.cpu()[torch.from_numpy(keep)], g[f"t{t}_x_out"][keep], what=f"{tag} frac t={t}")
         dl = close(lat.cpu(), g[f"t{t}_l_out"], what=f"{tag} lattice t={t}")
-        print(f"{tag} t={t}: types bit-exact ({N} atoms{ties}), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
+        same = "bit-exact" if not len(flipped) else f"{N - len(flipped)} of"
+        print(f"{tag} t={t}: types {same} ({N} atoms{ties}), max |dx| {dx:.2e}, lattice scaled err {dl:.2e}")
 
 
 def _t1_near_ties(model, g, nat, cn, flipped, ref_a):
