@@ -48,6 +48,7 @@ enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 // split16 edge GEMMs (edge16.hip): both operands split into fp16 hi/lo, stored per row as
 // [K/32][hi 32 | lo 32] (a 32-deep K-tile of a row = one 128-B line), three fp16 MFMA products,
 // staged by global_load_lds.
+constexpr int kRowInfo = 260;  // EdgeArgs::rinfo entries per row tile (a tile holds at most 257 nodes)
 struct EdgeArgs {
   long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M)
   long row_base;
@@ -78,6 +79,10 @@ struct EdgeArgs {
   // one counter per column group of 64; msgbuf [P][r2tot][H]: the continued rows, written only when
   // tile t-1 has not published in time). null rtiles = node tiles (tiles / ntiles).
   const int4* rtiles; float* sbuf; float* msgbuf; unsigned* rcnt; long r2tot;
+  // fc row tiles: each tile's node list as the segment-mean epilogue uses it, built on the host with the
+  // batch (rinfo [ntiles][kRowInfo] {node, rows | first row << 10 | kind << 20}, rinfo_n [ntiles] entries),
+  // so the epilogue loads it in one round trip instead of deriving it through dependent loads; or null
+  const int2* rinfo; const int* rinfo_n;
   // k_edge16_layer (both edge layers in one grid): per row tile, the count of layer-1 column tiles that
   // have written S through, then of the layer-2 tiles that have read it (the last one resets it to 0)
   unsigned* lflags;

@@ -27,6 +27,13 @@ namespace chm {
 
 #include "edge_common.h"
 
+// the segment-mean epilogue reads its row tile's node list from the host-built table (EdgeArgs::rinfo)
+// instead of deriving it through dependent loads (A/B builds: -DCHM_SEG_TABLE=0)
+#ifndef CHM_SEG_TABLE
+#define CHM_SEG_TABLE 1
+#endif
+constexpr bool kSegTable = CHM_SEG_TABLE;
+
 namespace {
 
 __device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
@@ -458,19 +465,26 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
 
   if constexpr (EPI == EPI_EDGE) {
     // S[c][e] = SiLU(D f + P_c[i] + Q_c[j]) as scaled hi/lo fp16 split rows (the P / Q rows of the
-    // tile's <= 8 source atoms and 1-2 crystals staged in LDS). First undo the W row scales.
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] *= sc;
-    }
+    // tile's <= 8 source atoms and 1-2 crystals staged in LDS).
     const int PQ_ROWS = LDS_B / (PQ_PITCH * 4);
-    const long rl = row0 + nrows - 1;
-    const int ilo = g.ei[row0], ihi = g.ei[rl];
-    const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
-    const int jlo = g.node_off[glo], jhi = g.node_off[ghi] + g.natoms[ghi] - 1;
-    const int nP = ihi - ilo + 1, nQ = jhi - jlo + 1, nR = nP + nQ;
+    // the tile's source-node range [ilo, ilo + nP) and target rows [jlo, jlo + nR - nP): pre-staging
+    // blocks took them before the main loop (SGPRs); the others load them here (a chain of four
+    // dependent loads, ~1 us each under load, that would otherwise open every pre-staged epilogue)
+    int ilo, jlo, nP, nR;
+    if (pre) {
+      ilo = p_ilo;
+      jlo = p_jlo;
+      nP = p_nP;
+      nR = p_nR;
+    } else {
+      const long rl = row0 + nrows - 1;
+      ilo = g.ei[row0];
+      const int ihi = g.ei[rl];
+      const int glo = g.n2g[ilo], ghi = g.n2g[ihi];
+      jlo = g.node_off[glo];
+      nP = ihi - ilo + 1;
+      nR = nP + g.node_off[ghi] + g.natoms[ghi] - jlo;
+    }
     const bool staged = pre || nR <= PQ_ROWS;
     const bool both = pre || (staged && g.npairs * nR <= PQ_ROWS);
     const float* T = reinterpret_cast<const float*>(lds + PQ_OFF);
@@ -486,6 +500,13 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         pr[i] -= ilo;
         qr[i] = nP + qr[i] - jlo;
       }
+    }
+    // undo the W row scales (after the row-index loads above are issued: their latency runs under these)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] *= sc;
     }
     auto stage = [&](int c0, int c1) __attribute__((always_inline)) {  // conditionings [c0, c1), each at rows [rb, rb + nR)
       if (pre) return;                 // (staged by the main loop's last tiles)
@@ -635,7 +656,11 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     int2* info = reinterpret_cast<int2*>(lds + SEG_B);
     int nn;
     int2 my = {0, 0};
-    if (g.rtiles) {
+    if (kSegTable && g.rinfo) {
+      // the host-built list: two independent loads, consumed only after the bias + SiLU pass below
+      nn = g.rinfo_n[rtile];
+      if (tid < kRowInfo) my = g.rinfo[rtile * kRowInfo + tid];
+    } else if (g.rtiles) {
       const int4 rt = g.rtiles[rtile];
       const long e0 = rtile * BM, e1 = e0 + nrows;
       const int nreg = rt.y - rt.x;

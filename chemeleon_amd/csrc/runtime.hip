@@ -101,6 +101,8 @@ struct chm_batch {
   // fc batches: edge layer 2 (k_edge16) on row tiles of exactly 256 edge rows, nodes cut at the tile
   // ends (EdgeArgs::rtiles); null for knn batches
   int4* rtiles = nullptr;
+  int2* rinfo = nullptr;    // per row tile: its node list (EdgeArgs::rinfo), and its length
+  int* rinfo_n = nullptr;
   long nrt = 0, r2tot = 0;  // row tiles; rows of the nodes continued from a previous tile
   float *sbuf = nullptr, *msgbuf = nullptr;
   unsigned* rcnt = nullptr;
@@ -478,6 +480,8 @@ struct BatchTables {
   std::vector<long> eoff, estart, coff;
   std::vector<int2> tiles;
   std::vector<int4> rtiles;  // fc: row tiles of edge layer 2 (EdgeArgs::rtiles)
+  std::vector<int2> rinfo;   // fc: the row tiles' node lists (EdgeArgs::rinfo, kRowInfo per tile)
+  std::vector<int> rinfo_n;
   long nrt = 0, r2tot = 0;
   long N = 0, E = 0;  // knn: E = the edge capacity
   long C = 0;         // knn: candidate scratch entries (sum of n^2 * 27)
@@ -552,6 +556,35 @@ static long row_tiles(const BatchTables& t, std::vector<int4>* out) {
   return r2tot;
 }
 
+// The node list of every row tile, exactly as edge16.hip's segment-mean epilogue would derive it from
+// rtiles / node_estart / node_n: {node, rows in the tile | first row in the tile << 10 | kind << 20},
+// kind 0 = a whole node, 1 = the head part of a node cut at the tile end (listed first), 2 = the rest of
+// a node begun in the previous tile (listed last). Unused entries are zero.
+static void row_tile_nodes(BatchTables& t) {
+  const long nrt = (long)t.rtiles.size(), E = t.E;
+  t.rinfo.assign((size_t)nrt * kRowInfo, make_int2(0, 0));
+  t.rinfo_n.assign(nrt, 0);
+  for (long k = 0; k < nrt; ++k) {
+    const int4 rt = t.rtiles[k];
+    const long e0 = k * kTileRows, e1 = e0 + (E - e0 < kTileRows ? E - e0 : kTileRows);
+    const int nreg = rt.y - rt.x;
+    const bool head = nreg > 0 && t.estart[rt.y - 1] + t.nn[rt.y - 1] > e1;
+    const bool cont = rt.z >= 0;
+    const int nn = nreg + (cont ? 1 : 0);
+    int2* o = t.rinfo.data() + (size_t)k * kRowInfo;
+    for (int i = 0; i < nn; ++i) {
+      if (cont && i == nn - 1) {
+        o[i] = make_int2(rt.z, (int)(t.estart[rt.z] + t.nn[rt.z] - e0) | (2 << 20));
+      } else {
+        const int v = rt.x + (head ? (i == 0 ? nreg - 1 : i - 1) : i);
+        const long es = t.estart[v], end = es + t.nn[v];
+        o[i] = make_int2(v, (int)((end > e1 ? e1 : end) - es) | ((int)(es - e0) << 10) | ((head && i == 0) ? 1 << 20 : 0));
+      }
+    }
+    t.rinfo_n[k] = nn;
+  }
+}
+
 // fills the per-node / per-edge tables (only when the batch is really built)
 static void batch_fill(BatchTables& t) {
   const int B = (int)t.nat.size();
@@ -593,6 +626,7 @@ static void batch_fill(BatchTables& t) {
   t.tiles.push_back(make_int2(cur0, (int)N));
   t.r2tot = row_tiles(t, &t.rtiles);
   t.nrt = (long)t.rtiles.size();
+  row_tile_nodes(t);
 }
 
 // number of segment tiles without building the tables (sizing only)
@@ -632,6 +666,8 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->tiles = (int2*)carve(ntiles * sizeof(int2));
   if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
     b->rtiles = (int4*)carve(b->nrt * sizeof(int4));
+    b->rinfo = (int2*)carve((size_t)b->nrt * kRowInfo * sizeof(int2));
+    b->rinfo_n = (int*)carve(b->nrt * sizeof(int));
     b->sbuf = fl((size_t)P * b->nrt * H);
     b->msgbuf = fl((size_t)P * (b->r2tot + 1) * H);
     b->rcnt = (unsigned*)carve((size_t)P * b->nrt * 8 * sizeof(unsigned));
@@ -749,6 +785,8 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->node_n, t.nn.data(), t.N * sizeof(int));
     up(b->tiles, t.tiles.data(), t.tiles.size() * sizeof(int2));
     up(b->rtiles, t.rtiles.data(), t.rtiles.size() * sizeof(int4));
+    up(b->rinfo, t.rinfo.data(), t.rinfo.size() * sizeof(int2));
+    up(b->rinfo_n, t.rinfo_n.data(), t.rinfo_n.size() * sizeof(int));
     if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
     if (e == hipSuccess && b->lflags) e = hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s);
@@ -1122,6 +1160,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
       if (m->edge_rows && b->rtiles) {  // 256-row tiles, cut nodes continued across tiles
         e2.rtiles = b->rtiles; e2.ntiles = (int)b->nrt; e2.sbuf = b->sbuf; e2.msgbuf = b->msgbuf;
+        e2.rinfo = b->rinfo; e2.rinfo_n = b->rinfo_n;
         e2.rcnt = b->rcnt; e2.r2tot = b->r2tot;
       }
       // (instrumented eager launches keep one launch per layer, so the per-kernel timings stay whole;
