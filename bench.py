@@ -233,8 +233,9 @@ def _run_pmc_pass(counter, outdir, argv, limit_s):
     import shutil
     import signal
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
-    cmd = [prof, "--pmc", counter, "-d", outdir, "-o", counter.lower(), "--output-format", "csv", "--",
-           sys.executable, os.path.abspath(__file__), "--traffic-probe"] + argv
+    cmd = [prof, "--pmc"] + counter.split() + ["-d", outdir, "-o", counter.split()[0].lower(), "--output-format",
+                                                "csv", "--", sys.executable, os.path.abspath(__file__),
+                                                "--traffic-probe"] + argv
     env = dict(os.environ, TMPDIR="/tmp")
     log = open(os.path.join(outdir + ".log"), "w")
     p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
@@ -266,12 +267,21 @@ def measure_traffic(args, kernel_key, limit_s=240):
     ks = traffic(os.path.join(root, "fetch_size"), os.path.join(root, "write_size"))
     for name, v in ks.items():
         if kernel_key in name and v["read_bytes"] is not None and v["write_bytes"] is not None:
-            return v["bytes_per_launch"], {
-                "source": f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 2-step eager "
-                          f"probe of the same workload ({name}, {v['launches']} launches)",
-                "read_bytes": v["read_bytes"], "write_bytes": v["write_bytes"],
-                "box": box_id(getattr(torch.cuda.get_device_properties(0), "uuid", None)),
-                "seconds": time.perf_counter() - t0}
+            src = {"source": f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 2-step eager "
+                             f"probe of the same workload ({name}, {v['launches']} launches)",
+                   "read_bytes": v["read_bytes"], "write_bytes": v["write_bytes"],
+                   "box": box_id(getattr(torch.cuda.get_device_properties(0), "uuid", None))}
+            # a third pass: MFMA busy share of the dominant kernel (SQ_VALU_MFMA_BUSY_CYCLES over all SIMDs
+            # against GRBM_GUI_ACTIVE, the sum over the 8 XCDs of their active cycles: 1024 SIMDs x GRBM / 8)
+            d = os.path.join(root, "mfma")
+            if _run_pmc_pass("SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE", d, argv, limit_s) == 0:
+                from chemeleon_amd.pmc import per_kernel
+                busy = [x for k, xs in per_kernel(d, "SQ_VALU_MFMA_BUSY_CYCLES").items() if kernel_key in k for x in xs]
+                act = [x for k, xs in per_kernel(d, "GRBM_GUI_ACTIVE").items() if kernel_key in k for x in xs]
+                if busy and act and sum(act) > 0:  # (per_kernel scales by 1024 for KiB counters: cancels here)
+                    src["mfma_busy"] = sum(busy) / (1024.0 * sum(act) / 8.0)
+            src["seconds"] = time.perf_counter() - t0
+            return v["bytes_per_launch"], src
     return None, {"error": f"no {kernel_key} dispatch in the PMC output", "dir": root}
 
 
@@ -565,6 +575,9 @@ def main():
                      "frac": ((lay_tflops if nlay else msg_tflops) / peak) if (lay_tflops or msg_tflops) else None,
                      "traffic": traffic,
                      "traffic_source": traffic_src,
+                     "mfma_busy": (traffic_src.get("mfma_busy") if isinstance(traffic_src, dict) else None),
+                     "mfma_busy_note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), in-run PMC "
+                                       "pass over the same probe as traffic",
                      "traffic_algorithmic": (edge_layer_bytes(natoms) if nlay else None),
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
                                    "split16": "fp32-equivalent flops (3 fp16 MFMA products each); fp16 dense MFMA "

@@ -18,6 +18,8 @@ print(f"{j['value']:.3f} {j['unit']}  {j['ms_per_step']:.2f} ms/step  "
       f"L2 {f(l2.get('avg_ms'), '.3f')} ms  L1 {f(l1.get('avg_ms'), '.3f')} ms  "
       f"path {j['path']['tflops']:.0f} TF")
 extra = []
+if r.get("mfma_busy") is not None:
+    extra.append(f"MFMA busy {r['mfma_busy']:.3f}")
 if r.get("traffic"):
     extra.append(f"traffic {r['traffic'] / 1e9:.2f} GB/launch"
                  + (f" ({r['traffic'] / r['traffic_algorithmic']:.2f}x alg)" if r.get("traffic_algorithmic") else ""))
