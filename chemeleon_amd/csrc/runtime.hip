@@ -813,6 +813,24 @@ extern "C" int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out) {
   return CHM_OK;
 }
 
+extern "C" int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2, int64_t cap2, int32_t* counts,
+                                   int64_t cap) {
+  if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
+  BatchTables t;
+  int rc = batch_tables(h_natoms, B, t);
+  if (rc) return rc;
+  batch_fill(t);
+  const long R = (long)t.rtiles.size();
+  if (out2 && cap2 >= 2 * (int64_t)t.rinfo.size())
+    for (size_t k = 0; k < t.rinfo.size(); ++k) {
+      out2[2 * k] = t.rinfo[k].x;
+      out2[2 * k + 1] = t.rinfo[k].y;
+    }
+  if (counts && cap >= R)
+    for (long k = 0; k < R; ++k) counts[k] = t.rinfo_n[k];
+  return (int)R;
+}
+
 extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
   if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   BatchTables t;

@@ -281,6 +281,9 @@ int chm_debug_d3pm_philox(int N, int A, int T, const float* d_logits, const int6
  * first node starting after it, the node continued from the previous tile or -1, that node's row
  * offset in the continued-rows buffer}, and *r2tot the buffer's rows. */
 int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot);
+/* (host only) the row tiles' node lists (EdgeArgs::rinfo: kRowInfo = 260 {node, packed} pairs per tile) and
+ * their lengths, as edge layer 2's segment-mean epilogue reads them; returns the number of row tiles */
+int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2, int64_t cap2, int32_t* counts, int64_t cap);
 /* Host-only test hook: the block -> job map of the one-grid edge-layer kernel (k_edge16_layer) for R
  * row tiles, P conditionings and layer-2 lag `lag`. Returns the grid size nb (or a negative CHM_E_*);
  * if out holds >= 2 nb int64 it receives per block {kind (0 none, 1 edge layer 1, 2 edge layer 2),

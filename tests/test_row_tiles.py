@@ -4,6 +4,7 @@ from its crystal's offset + i n), the nodes that start in it, the node continued
 tile and that node's offset in the continued-rows buffer. Checked against a direct Python
 construction on uniform, ragged and degenerate batches."""
 
+import collections
 import ctypes
 
 import numpy as np
@@ -62,6 +63,65 @@ def test_row_tiles_match_direct_construction(natoms):
     assert listed == list(range(N))
     conts = [c for _, _, c, _ in got if c >= 0]
     assert len(conts) == len(set(conts))
+
+
+def reference_nodes(natoms):
+    """Each row tile's node list as edge16.hip's segment-mean epilogue derived it on the device before the
+    host-built table (EdgeArgs::rinfo): {node, rows in the tile | first row << 10 | kind << 20}, kind 0 = a
+    whole node, 1 = the head part of a node cut at the tile end (listed first), 2 = the rest of a node
+    begun in the previous tile (listed last)."""
+    tiles, _ = reference_tiles(natoms)
+    starts, nn = [], []
+    e = 0
+    for n in natoms:
+        for _ in range(n):
+            starts.append(e)
+            nn.append(n)
+            e += n
+    E = e
+    out = []
+    for t, (x, y, c, _) in enumerate(tiles):
+        e0 = 256 * t
+        e1 = e0 + min(E - e0, 256)
+        nreg = y - x
+        head = nreg > 0 and starts[y - 1] + nn[y - 1] > e1
+        lst = []
+        for i in range(nreg):
+            v = x + ((nreg - 1 if i == 0 else i - 1) if head else i)
+            es, end = starts[v], starts[v] + nn[v]
+            lst.append((v, (min(end, e1) - es) | ((es - e0) << 10) | ((1 << 20) if head and i == 0 else 0)))
+        if c >= 0:
+            lst.append((c, (starts[c] + nn[c] - e0) | (2 << 20)))
+        out.append(lst)
+    return out
+
+
+@pytest.mark.parametrize("natoms", [
+    [40] * 64, [20] * 64, [6] * 4, [80] * 9, [1] * 600, [16] * 16, [256], [1, 255, 2, 80, 3],
+    np.random.default_rng(7).integers(1, 81, 300).tolist(),
+])
+def test_row_tile_node_lists(natoms):
+    """The host-built node lists (chm_debug_row_nodes, the table edge layer 2's epilogue reads) equal the
+    device's former derivation, restated here from the tile table, node starts and degrees; every
+    node's rows are covered exactly once across its head and continued parts."""
+    lib = _lib.load()
+    nat = (ctypes.c_int32 * len(natoms))(*natoms)
+    R = lib.chm_debug_row_nodes(nat, len(natoms), None, 0, None, 0)
+    assert R > 0, lib.chm_last_error()
+    K = 260
+    out = (ctypes.c_int32 * (2 * K * R))()
+    cnt = (ctypes.c_int32 * R)()
+    assert lib.chm_debug_row_nodes(nat, len(natoms), out, 2 * K * R, cnt, R) == R
+    want = reference_nodes(natoms)
+    assert len(want) == R
+    rows = collections.Counter()
+    for t in range(R):
+        got = [(out[2 * (t * K + i)], out[2 * (t * K + i) + 1]) for i in range(cnt[t])]
+        assert got == want[t], f"tile {t}"
+        assert all(out[2 * (t * K + i)] == 0 and out[2 * (t * K + i) + 1] == 0 for i in range(cnt[t], K))
+        for v, w in got:
+            rows[v] += w & 1023
+    assert all(rows[v] == n for v, n in enumerate(n for n in natoms for _ in range(n)))
 
 
 def test_row_tiles_reject_bad_batches():
