@@ -76,6 +76,10 @@ def parse():
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the in-run HBM traffic measurement of the dominant kernel (two rocprofv3 --pmc passes "
                         "over a 2-step eager probe; roofline.traffic then falls back to the committed profile)")
+    p.add_argument("--noise", choices=["philox", "torch"], default="philox",
+                   help="philox: device noise keyed by global index (the headline); torch: parity mode, the "
+                        "reference's CPU RNG stream drawn on every rank at the global size, each rank uploading its "
+                        "rows before every replay of the captured step (chemeleon_amd.noise)")
     p.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)  # (the PMC passes' workload)
     return p.parse_args()
 
@@ -415,9 +419,26 @@ def main():
         dist.broadcast(null, 0)
 
     model.decoder.set_math(args.math)
-    it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
-                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
-                             graph=not args.no_graph, lanes=args.lanes)
+    draw_ms = None
+    if args.noise == "torch":
+        # parity mode: every rank seeds the CPU generator alike and draws the whole job's tensors (initial
+        # state and per-step noise), keeping its rows; the per-step host draw of this rank's share, timed alone
+        from chemeleon_amd.noise import StepNoise
+        sn = StepNoise(sum(all_nat), total, A, node_base, node_base + sum(natoms), g0, g0 + len(natoms))
+        bufs = tuple(torch.empty(sh).pin_memory() for sh in sn.local_shapes)
+        sn.draw(out=bufs)
+        t0 = time.perf_counter()
+        for _ in range(10):
+            sn.draw(out=bufs)
+        draw_ms = (time.perf_counter() - t0) / 10 * 1e3
+        torch.manual_seed(args.seed)
+        it = model.sample_states(natoms, None, 2.0, 1e-5, noise="torch", text_embeds=cond, null_text_embeds=null,
+                                 clone=False, node_base=node_base, graph_base=g0,
+                                 global_sizes=(sum(all_nat), total), graph=not args.no_graph)
+    else:
+        it = model.sample_states(natoms, None, 2.0, 1e-5, noise="philox", seed=args.seed, text_embeds=cond,
+                                 null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
+                                 graph=not args.no_graph, lanes=args.lanes)
     next(it)  # initial state
     _lib.prof_events(reset=True)  # edge-kernel health counters (wait timeouts, repairs) from here on
     # per-kernel HIP-event instrumentation (eager launches only; graph captures are not instrumented)
@@ -493,8 +514,7 @@ def main():
     math = model.decoder.get_math()
     fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
-    edge16 = os.environ.get("CHM_EDGE16", "1") != "0"
-    msg_kernel = "k_edge16_layer" if nlay else ("k_edge16<2" if edge16 else "k_edge_gemm<2")
+    msg_kernel = "k_edge16_layer" if nlay else "k_edge16<2"
     traffic, traffic_src = None, "not collected for the ragged workload" if args.ragged else "not collected"
     if math == "split16" and not args.ragged:
         if rank == 0 and world == 1 and not args.no_traffic:
@@ -557,7 +577,10 @@ def main():
                                f"T={T_STEPS}; step = one reverse timestep (4 decoder calls)",
                    "n_samples": total, "n_atoms": "ragged 1-80" if args.ragged else args.n_atoms,
                    "timesteps": T_STEPS,
-                   "parallelism": f"sample-sharded x{world}", "noise": "philox (device)",
+                   "parallelism": f"sample-sharded x{world}",
+                   "noise": ("philox (device)" if args.noise == "philox" else
+                             "torch (parity mode: the reference's CPU RNG stream at the global size on every rank, "
+                             "this rank's rows uploaded before each replay)"),
                    "launch": "eager" if args.no_graph else f"hip graph replay per step, {args.lanes} stream lane(s)"},
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
@@ -567,7 +590,7 @@ def main():
                                             "both conditionings, incl. its two repair launches (no-ops unless a "
                                             "check fails)") if nlay else
                                            (f"edge message GEMM + fused scatter_mean ({msg_kernel}, EPI_SEGMEAN, "
-                                            f"{'16x16x32' if edge16 else '32x32x16'} MFMA), both conditionings"),
+                                            "16x16x32 MFMA), both conditionings"),
                                 "bf16x3": "edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), "
                                           "both conditionings",
                                 "f32": "edge message GEMM (k_gemm, S.W2^T + SiLU, both conditionings)"}[math],
@@ -605,6 +628,7 @@ def main():
                  "math": math, "flops_per_step_per_gpu": step_flops,
                  "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,
                  "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
+        "noise_host_draw_ms": draw_ms,
         "edge_repairs": events["layer_repairs"] + events["tail_repairs"],
         "edge_events": dict(events, note="device counters over warm-up, timed and eager passes (chm_prof_events): "
                                          "repairs recompute a layer whose intra-grid check failed; 0 = none ran"),

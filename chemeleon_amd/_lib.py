@@ -104,6 +104,8 @@ SIGNATURES = {
     "chm_prof_read": (c_int, [c_int, ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_double)]),
     "chm_prof_events": (c_int, [ctypes.POINTER(c_i64), c_int]),
     "chm_prof_events_reset": (c_int, []),
+    "chm_mt19937_uniform": (c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
+                                    ctypes.POINTER(ctypes.c_int32), c_i64, c_i64, c_i64, c_void_p]),
 }
 
 
@@ -166,7 +168,8 @@ def prof_read(kernel: int):
     return int(n.value), float(ms.value)
 
 
-EVENT_NAMES = ("layer_wait_timeouts", "layer_other_xcd", "layer_repairs", "tail_wait_timeouts", "tail_repairs")
+EVENT_NAMES = ("layer_wait_timeouts", "layer_other_xcd", "layer_repairs", "tail_wait_timeouts", "tail_repairs",
+               "layer_incomplete")
 
 
 def prof_events(reset: bool = False):

@@ -20,7 +20,7 @@ DEFS = os.environ.get("CHM_BUILD_DEFS", "").split()
 if os.environ.get("CHM_BUILD_LIB"):
     LIB = os.path.abspath(os.environ["CHM_BUILD_LIB"])
     LIBDIR = os.path.dirname(LIB)
-SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "split16.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip"]
+SOURCES = ["kernels.hip", "gemm_bf16x3.hip", "split16.hip", "edge16.hip", "node_gemm.hip", "knn.hip", "runtime.hip", "host_noise.cpp"]
 ARCH = os.environ.get("CHM_OFFLOAD_ARCH", "gfx950")
 
 
@@ -45,7 +45,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     from concurrent.futures import ThreadPoolExecutor
 
     def compile_one(src):
-        obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src),
                "-o", obj, "-Wno-unused-result"] + DEFS
         if verbose:

@@ -10,6 +10,7 @@ constexpr int NF = 128;      // num_freqs
 constexpr int FD = 6 * NF;   // Fourier feature width, 768
 constexpr int TD = 128;      // time_dim
 constexpr int HEADS_N = 128; // type_out (A <= 125) + coord_out (3) packed, padded
+constexpr int kMaxLayers = 64;  // num_layers accepted by chm_model_create
 
 // C[M,N] = epi(A[M,K] . W[N,K]^T), fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32.
 struct GemmArgs {
@@ -110,7 +111,9 @@ struct EdgeArgs {
 // until chm_prof_events_reset: wait timeouts and repair launches that ran (each must read 0 in a
 // healthy run; a repair doubles the cost of its layer).
 enum { EV_LAYER_TIMEOUT = 0, EV_LAYER_XCD = 1, EV_LAYER_REPAIR = 2, EV_TAIL_TIMEOUT = 3, EV_TAIL_REPAIR = 4,
-       EV_COUNT = 8 };
+       EV_LAYER_INCOMPLETE = 5, EV_COUNT = 8 };
+// the XCD ids (bit x = XCC_ID x) the blocks of a `blocks`-block grid ran on (synchronous; model creation)
+hipError_t xcd_mask(int blocks, unsigned* out);
 hipError_t edge_events_read(unsigned long long* out);  // EV_COUNT values
 hipError_t edge_events_reset();
 // knn (radius-graph) edges, knn.hip: per-crystal scratch at cand_off[b] (n^2 * 27 entries; the final
@@ -150,7 +153,7 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_g
 // sched != null: the persistent form (grid blocks; the last pool% of the row tiles claimed at run time;
 // sched = the layer's zeroed scheduling words, 16 + 8 * cap, cap >= R + lag + 64)
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s,
-                             unsigned* sched = nullptr, int cap = 0, int grid = 0, int pool = 15);
+                             unsigned* sched = nullptr, int cap = 0, int grid = 0, int pool = 15, int skip_xcd = -1);
 void edge16_seq_jobs(long n, int P, int D, long* out);  // (host) the persistent form's per-XCD job sequence
 long edge16_layer_blocks(long R, int P);                        // its grid size
 void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map

@@ -914,12 +914,15 @@ __device__ __forceinline__ unsigned wait_slot(const unsigned* p, bool& late) {
 // (A static row's job costs only the XCD counter's atomic, about what the hardware dispatch of a block
 // of the static map costs; claiming every row from the pool measured slower: 512x40 58.15 vs 57.9 ms
 // per step at edge_pool 30 vs 15.)
+// skip_x >= 0 (tests only, option edge_dyn_skip_xcd): the blocks on XCD skip_x exit at once, as if that
+// XCD did not exist, so the self-check below must catch it.
 __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeArgs g2, int R, int D, unsigned* sched,
-                                                             int cap, int ns) {
+                                                             int cap, int ns, int skip_x) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const unsigned x = xcc_id();
   const int P = g2.npairs;
   unsigned* slots = sched + 16 + (long)x * cap;  // local row ns + i -> slots[i]
+  unsigned long long* done = reinterpret_cast<unsigned long long*>(sched + 10);  // finished layer-2 tiles | exits << 32
   int* bc = reinterpret_cast<int*>(lds);
   for (;;) {
     if (threadIdx.x == 0) {
@@ -929,7 +932,9 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeAr
       unsigned v = 0;  // the row + 1, ~0u = none
       bool late = false;
       const long jd = j.row - ns;  // pool slot of a local row past the static ones
-      if (jd >= cap) {
+      if ((int)x == skip_x) {
+        code = 0;
+      } else if (jd >= cap) {
         v = ~0u;  // (beyond every possible row: its layer-2 row is invalid too)
       } else if (jd < 0) {
         v = (unsigned)(x * ns + j.row) + 1u;
@@ -946,12 +951,27 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeAr
         if (v == 0u) v = ~0u;
       }
       long bid = 0;
-      if (j.kind == 1) {
+      if ((int)x == skip_x) {
+      } else if (j.kind == 1) {
         code = v == ~0u ? 3 : 1;
         bid = (long)(v - 1u) * 2 + j.sub;
       } else {
         code = v == ~0u ? 0 : 2;
         bid = ((long)(v - 1u) * P + j.sub / 2) * 2 + (j.sub & 1);
+      }
+      if (code == 0) {
+        // Exit. Self-check: the static rows of an XCD that does not exist (a device or
+        // partition mode with fewer than 8 XCDs) would never be computed. Layer-2 tiles add 1 to
+        // done[0] as they finish and exiting blocks add 2^32; the last block out sees every finished
+        // tile in the same word (one location: its coherence order holds every block's finish before
+        // its exit) and raises the repair request if any layer-2 tile is missing.
+        const unsigned long long old = __hip_atomic_fetch_add(done, 1ull << 32, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        if ((old >> 32) + 1ull == (unsigned long long)gridDim.x &&
+            (old & 0xffffffffull) != (unsigned long long)R * P * 2) {
+          __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          count_event(EV_LAYER_INCOMPLETE);
+        }
       }
       if (late) {  // (never in a healthy run: the layer is recomputed by the repair launches)
         __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -981,7 +1001,27 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeAr
     else
       edge16_tile<EPI_SEGMEAN, true, true>(*a2, vb, 0, bid, tid);
     __syncthreads();
+    if (code == 2 && threadIdx.x == 0) __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// The XCDs a grid's blocks run on (bit x = XCC_ID x), for the persistent kernel's 8-XCD assumption.
+__global__ void k_xcd_probe(unsigned* mask) {
+  if (threadIdx.x == 0) atomicOr(mask, 1u << xcc_id());
+}
+
+hipError_t xcd_mask(int blocks, unsigned* out) {
+  unsigned* d = nullptr;
+  hipError_t e = hipMalloc(&d, sizeof(unsigned));
+  if (e != hipSuccess) return e;
+  e = hipMemset(d, 0, sizeof(unsigned));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_xcd_probe, dim3((unsigned)blocks), dim3(64), 0, 0, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d, sizeof(unsigned), hipMemcpyDeviceToHost);
+  hipFree(d);
+  return e;
 }
 
 // Repair of a k_edge16_layer launch whose check failed (*g.xbad != 0: some layer-2 tile read S written
@@ -989,14 +1029,18 @@ __global__ __launch_bounds__(512, 1) void k_edge16_layer_dyn(EdgeArgs g1, EdgeAr
 // stride over the tiles so that the normal case (nothing to repair) costs one small grid that exits.
 // The layer-1 pass also clears the layer's agg row maxima (the failed launch may have max-ed garbage).
 // ev >= 0: count the repair (block 0) as that event.
+// (The layer-1 pass also clears the row-tile partial-sum counters rcnt: when a launch ended with tiles
+// that never ran, k_edge16_layer_dyn with an XCD missing, a head tile's count has no partner left.)
 template <int EPI, bool ASC>
 __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, unsigned* agg_max, long nmax,
-                                                          unsigned* lflags, long nrt, int ev) {
+                                                          unsigned* lflags, long nrt, int ev, unsigned* rcnt = nullptr,
+                                                          long nrcnt = 0) {
   if (__hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   if (ev >= 0 && blockIdx.x == 0 && threadIdx.x == 0) count_event(ev);
   if (EPI == EPI_EDGE && agg_max) {  // (and the row-tile flags, in case a wait timed out)
     for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
     for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrt; k += (long)gridDim.x * 512) lflags[k] = 0u;
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrcnt; k += (long)gridDim.x * 512) rcnt[k] = 0u;
   }
   for (long vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     edge16_tile<EPI, ASC>(g, vb, nvb);
@@ -1004,7 +1048,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, 
   }
 }
 
-hipError_t edge16_init() {
+static hipError_t edge16_init_once() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
@@ -1014,6 +1058,12 @@ hipError_t edge16_init() {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// the kernels' LDS attribute, set once per process (thread-safe: a function-local static initialiser)
+hipError_t edge16_init() {
+  static const hipError_t e = edge16_init_once();
+  return e;
 }
 
 hipError_t edge_events_read(unsigned long long* out) {
@@ -1036,12 +1086,7 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_g
       !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale ||
       (g2.rtiles && (!g2.sbuf || !g2.msgbuf || !g2.rcnt || (long)g2.ntiles * BM < g2.E)))
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = edge16_init();
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   const long nt1 = ((g1.M - g1.row_base + BM - 1) / BM) * (g1.N / BN);
   const long nb1 = (nt1 + 7) / 8 * 8;
   const long nt2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
@@ -1084,7 +1129,7 @@ void edge16_seq_jobs(long n, int P, int D, long* out) {
 }
 
 hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, int repair_grid, hipStream_t s,
-                             unsigned* sched, int cap, int grid, int pool) {
+                             unsigned* sched, int cap, int grid, int pool, int skip_xcd) {
   if (g1.N != H || g1.K % (2 * BK) || g1.aexp || !g1.S || !g1.sexp || !g1.PQ || !g1.node_off || !g1.natoms ||
       !g1.n2g || !g1.A || !g1.W || !g1.wscale || g1.npairs > 2 || g1.row_base != 0 || g1.flags || !g1.lflags ||
       !g1.xbad || g1.xbad != g2.xbad)
@@ -1094,18 +1139,13 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
       g2.npairs != g1.npairs || (long)g2.ntiles * BM < g2.E || (long)g2.ntiles * BM - g2.E >= BM || g1.M != g1.E ||
       lag < 1)
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = edge16_init();
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   const long R = g2.ntiles;
   if (sched) {  // persistent, the last rows claimed at run time (k_edge16_layer_dyn)
     if (grid < 1 || cap < R + lag + 64 || pool < 0 || pool > 100) return hipErrorInvalidValue;
     const int ns = (int)((R - (R * pool + 99) / 100) / 8);  // static rows per XCD
     hipLaunchKernelGGL(k_edge16_layer_dyn, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, (int)R, lag, sched, cap,
-                       ns);
+                       ns, skip_xcd);
   } else {
     const long blocks = edge16_layer_blocks(R, g2.npairs);
     hipLaunchKernelGGL(k_edge16_layer, dim3((unsigned)blocks), dim3(512), LDS_B, s, g1, g2, (int)R, lag);
@@ -1118,7 +1158,7 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
   const long nb1 = ((g1.M + BM - 1) / BM) * (g1.N / BN), nb2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
   const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
   hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, nb1, g2.agg_max,
-                     (long)g2.npairs * g2.nnodes, g1.lflags, R, -1);
+                     (long)g2.npairs * g2.nnodes, g1.lflags, R, -1, g2.rcnt, (long)g2.npairs * R * 8);
   hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nb2, (unsigned*)nullptr, 0L,
                      (unsigned*)nullptr, 0L, (int)EV_LAYER_REPAIR);
   return hipGetLastError();
@@ -1140,12 +1180,7 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
       return hipErrorInvalidValue;
     blocks = ((g.M - g.row_base + BM - 1) / BM) * (g.N / BN);
   }
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = edge16_init();
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   const EdgeArgs& ga = g;
   const dim3 grid((unsigned)blocks), block(512);
   if (epi == EPI_EDGE)

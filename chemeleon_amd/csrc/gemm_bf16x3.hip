@@ -484,7 +484,7 @@ static_assert((size_t)LBM * 132 * sizeof(float) <= kBigLds, "segment tile fits t
 
 // opt the large dynamic-LDS kernels in; called at model creation, outside any
 // stream capture (a function attribute call is not a stream operation)
-hipError_t gemm_init() {
+static hipError_t gemm_init_once() {
   const void* ks[] = {(const void*)k_gemm3_big<EPI_STD>, (const void*)k_gemm3_big<EPI_EDGE>,
                       (const void*)k_gemm3_big<EPI_SEGMEAN>};
   for (const void* k : ks) {
@@ -492,6 +492,12 @@ hipError_t gemm_init() {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// (set once per process; a function-local static initialiser is thread-safe)
+hipError_t gemm_init() {
+  static const hipError_t e = gemm_init_once();
+  return e;
 }
 
 hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) {
@@ -504,12 +510,7 @@ hipError_t gemm_bf16x3_big(const GemmArgs& g, int epi, hipStream_t s) {
     if (g.M <= 0) return hipErrorInvalidValue;
     blocks = ((g.M + LBM - 1) / LBM) * (g.N / LBN);
   }
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = gemm_init();
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (hipError_t e = gemm_init(); e != hipSuccess) return e;
   if (epi == EPI_EDGE)
     hipLaunchKernelGGL((k_gemm3_big<EPI_EDGE>), dim3((unsigned)blocks), dim3(512), kBigLds, s, g);
   else if (epi == EPI_SEGMEAN)

@@ -352,7 +352,7 @@ int g_node_variant = 0;
 constexpr int LDS3 = STB<true> * NST<true, 3>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
 
-hipError_t node_gemm_init() {
+static hipError_t node_gemm_init_once() {
   const void* ks[10] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
                         (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
                         (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
@@ -361,6 +361,12 @@ hipError_t node_gemm_init() {
   const int bytes[10] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4};
   hipError_t e = hipSuccess;
   for (int i = 0; i < 10 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  return e;
+}
+
+// (set once per process; a function-local static initialiser is thread-safe)
+hipError_t node_gemm_init() {
+  static const hipError_t e = node_gemm_init_once();
   return e;
 }
 
@@ -375,12 +381,7 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   g.linear_order = linear;
   if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
   if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = node_gemm_init();
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  if (hipError_t e = node_gemm_init(); e != hipSuccess) return e;
   const long blocks = ((g.M + 127) / 128) * (g.N / NN);
   const dim3 grid((unsigned)blocks), block(256);
   const bool v1 = g_node_variant == 1;

@@ -26,6 +26,8 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+// (for the host-only entry points of other translation units, host_noise.cpp)
+int chm_fail_host(int code, const char* msg) { return fail(code, msg); }
 
 #define HIPCHK(expr)                                                                         \
   do {                                                                                       \
@@ -80,6 +82,8 @@ struct chm_model {
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int ncu = 0;           // compute units of the device the model lives on
+  unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
+  int edge_skip_xcd = -1;  // (tests) option edge_dyn_skip_xcd: the persistent kernel's blocks on that XCD exit
   int repair_grid = 0;   // CHM_REPAIR_GRID: blocks of the edge kernels' repair launches (default: ncu)
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
@@ -151,7 +155,7 @@ static int check_dims(const chm_dims* d) {
     return fail(CHM_E_UNSUPPORTED, "time_dim must be 128 in this build (or time_dim = text_dim = 0)");
   if (d->text_dim < 0 || (TD + d->text_dim) % 16) return fail(CHM_E_UNSUPPORTED, "time_dim + text_dim must be a multiple of 16");
   if (d->max_atoms < 1 || d->max_atoms + 3 > HEADS_N) return fail(CHM_E_UNSUPPORTED, "max_atoms must be in [1, 125]");
-  if (d->num_layers < 1 || d->num_layers > 64) return fail(CHM_E_ARG, "num_layers out of range");
+  if (d->num_layers < 1 || d->num_layers > kMaxLayers) return fail(CHM_E_ARG, "num_layers out of range");
   return CHM_OK;
 }
 
@@ -306,6 +310,9 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
+    // k_edge16_layer_dyn gives each of 8 XCDs static rows: on a device or partition mode with fewer XCDs
+    // it would leave rows to its self-check and repair launches, so it runs only where 8 were seen
+    if (m->ncu > 0 && xcd_mask(8 * m->ncu, &m->xcd_mask) != hipSuccess) m->xcd_mask = 0;
     struct Job { const float* src; size_t n; const void** dst; };
     std::vector<Job> jobs;
     jobs.push_back({m->Wc, (size_t)2 * H * CIN, &m->Wc3});
@@ -418,6 +425,15 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
   if (k == "edge_layer_dyn") {  // persistent one-grid kernel: 0 never, 1 from kDynMinTiles row tiles on, 2 always
     if (value < 0 || value > 2) return fail(CHM_E_ARG, "edge_layer_dyn must be 0, 1 or 2");
     m->edge_dyn = (int)value;
+    return CHM_OK;
+  }
+  if (k == "edge_dyn_skip_xcd") {  // (tests) the persistent kernel's blocks on XCD `value` exit at once (-1: none)
+    if (value < -1 || value > 7) return fail(CHM_E_ARG, "edge_dyn_skip_xcd must be in [-1, 7]");
+    m->edge_skip_xcd = (int)value;
+    return CHM_OK;
+  }
+  if (k == "xcd_mask") {  // (tests) override the XCD mask probed at creation
+    m->xcd_mask = (unsigned)value;
     return CHM_OK;
   }
   if (k == "edge_pool") {  // its run-time-claimed share of the row tiles, percent (0: static rows only)
@@ -672,7 +688,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->msgbuf = fl((size_t)P * (b->r2tot + 1) * H);
     b->rcnt = (unsigned*)carve((size_t)P * b->nrt * 8 * sizeof(unsigned));
     b->lflags = (unsigned*)carve(b->nrt * sizeof(unsigned));
-    b->xbad = (unsigned*)carve(64 * sizeof(unsigned));
+    b->xbad = (unsigned*)carve(2 * kMaxLayers * sizeof(unsigned));  // layer l: [l]; tail of layer l: [kMaxLayers + l]
     b->sched_cap = b->nrt + kMaxLag + 64;
     b->sched = (unsigned*)carve((size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned));
   }
@@ -1130,10 +1146,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
   }
   if (b->xbad && b->math == MATH_SPLIT16) {
-    // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[32 + l])
+    // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[kMaxLayers + l])
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)
-    HIPCHK(hipMemsetAsync(b->xbad, 0, 64 * sizeof(unsigned), s));
+    HIPCHK(hipMemsetAsync(b->xbad, 0, 2 * kMaxLayers * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
@@ -1194,10 +1210,11 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         HIPCHK(traced_edge_launch(m, e1, 3, E, s, [&] {
           e2.trace = e1.trace;
           const hipError_t r =
-              m->ncu > 0 && (m->edge_dyn == 2 || (m->edge_dyn == 1 && b->nrt >= kDynMinTiles))
+              m->ncu > 0 && m->xcd_mask == 0xffu &&
+                      (m->edge_dyn == 2 || (m->edge_dyn == 1 && b->nrt >= kDynMinTiles))
                   ? edge_gemm16_layer(e1, e2, m->edge_lag, m->repair_grid, s,
                                       b->sched + (size_t)l * (16 + 8 * b->sched_cap), (int)b->sched_cap, m->ncu,
-                                      m->edge_pool)
+                                      m->edge_pool, m->edge_skip_xcd)
                   : edge_gemm16_layer(e1, e2, m->edge_lag, m->repair_grid, s);
           e2.trace = nullptr;
           return r;
@@ -1214,7 +1231,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e1b.row_base = b->l1_rows_a;
         e1b.flags = e2.flags = b->tail_flags;
         e1b.flag_row0 = e2.flag_row0 = b->l1_rows_a;
-        e2.xbad = b->xbad + 32 + l;  // (a timed-out wait: the repair launches recompute edge layer 2)
+        e2.xbad = b->xbad + kMaxLayers + l;  // (a timed-out wait: the repair launches recompute edge layer 2)
         HIPCHK(edge_gemm16(e1, EPI_EDGE, s));
         HIPCHK(edge_gemm16_tail(e1b, e2, m->repair_grid, s));
       } else {

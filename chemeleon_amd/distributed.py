@@ -7,9 +7,14 @@ exchange:
   1. rank 0 computes the conditioning vectors once (the frozen text encoder)
      and broadcasts them (2 x [B, 512] fp32);
   2. every rank samples a contiguous range of crystals, balanced by edge work
-     (sum of n^2); device Philox noise is keyed by GLOBAL node / graph index,
-     so the result does not depend on the number of ranks;
+     (sum of n^2). The noise never depends on the number of ranks: in parity
+     mode (noise="torch", the reference's CPU RNG stream) every rank advances
+     the CPU generator over the global draws and keeps its own rows
+     (chemeleon_amd.noise); in perf mode (noise="philox") device Philox noise
+     is keyed by GLOBAL node / graph index;
   3. the finished structures are all-gathered (padded to the largest shard).
+Chemeleon.sample() takes this path by itself when torch.distributed is
+initialised over more than one rank.
 The reference has no distributed sampler (its Lightning DDP is training only,
 run.py:78-92); this module is the MI355X-native counterpart asked for by the
 north star.
@@ -108,35 +113,97 @@ def gather_states(states: Tuple[torch.Tensor, torch.Tensor, torch.Tensor], natom
     return A, X, LT, [n for ns in natoms_all for n in ns]
 
 
+def _world(group):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def _shared_conditioning(model, texts, B, cond, null, group):
+    """Conditioning vectors [B, text_dim] on every rank: the text encoder (or the given vectors) on
+    rank 0 only, then one broadcast of each (the north star's "computed once on host and
+    broadcast"). None for a model without text guidance."""
+    if not model.text_guide:
+        return None, None
+    world, rank = _world(group)
+    dev = model.device
+    if rank == 0 or world == 1:
+        c, n = model._conditioning(texts, B, cond, null)
+    else:  # receive buffers of the same shape (every rank knows B and text_dim)
+        d = model.hparams["text_dim"]
+        c = torch.zeros(B, d, device=dev)
+        n = torch.zeros(B, d, device=dev)
+    if cond is not None and cond.shape[0] not in (1, B):
+        raise ValueError(f"text_embeds has {cond.shape[0]} rows for {B} crystals")
+    return broadcast_conditioning(c, n, 0, group)
+
+
 @torch.no_grad()
-def sample_distributed(model, natoms: Sequence[int], cond: torch.Tensor, null: torch.Tensor, cond_scale=2.0,
-                       step_lr=1e-5, seed: int = 0, group=None, init: Optional[Tuple] = None):
-    """Sample `natoms` (global list) across all ranks; returns the global final
-    state (atom_types, frac_coords, lattices, natoms) on every rank.
-    `cond` / `null` are the [1 or B, text_dim] conditioning vectors held by
-    rank 0 (broadcast here)."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+def sample_states_distributed(model, natoms: Sequence[int], texts=None, cond_scale: float = 2.0,
+                              step_lr: float = 1e-5, *, noise: str = "torch", seed: int = 0, text_embeds=None,
+                              null_text_embeds=None, group=None, init: Optional[Tuple] = None,
+                              every_step=False, graph: Optional[bool] = None):
+    """Reverse loop over a GLOBAL crystal list, sharded across the ranks of `group`: yields
+    (t, atom_types, frac_coords, lattices) of the WHOLE batch on every rank, for every t
+    (every_step=True, one all-gather per step: the stream / return_trajectory case), for the t in
+    every_step (a collection of timesteps) and the final state, or only the final state t = 0
+    (every_step=False: one all-gather at the end; nothing is exchanged inside the loop).
+
+    noise="torch" (parity mode, the default of Chemeleon.sample): every rank advances the global CPU
+    generator over the reference's global draws (chemeleon.py:348-349, 400-404, 418, 435, 455) and
+    keeps its own rows, so the gathered result is bit-identical to the single-process run for any
+    rank count, provided every rank seeded its generator the same way (torch.manual_seed(s) before
+    the call, as for the reference). noise="philox": device noise keyed by (seed, t, global index);
+    the initial noise comes from Generator(seed) at the global size."""
+    world, rank = _world(group)
     natoms = [int(n) for n in natoms]
     # every rank holds the same list, so every rank raises here, before any collective
     if len(natoms) < world:
         raise ValueError(f"{len(natoms)} crystals cannot be sharded over {world} ranks (one crystal at least per rank)")
+    if noise not in ("torch", "philox"):
+        raise ValueError("noise must be 'torch' or 'philox'")
     ranges = partition(natoms, world)
     g0, g1 = ranges[rank]
-    cond, null = broadcast_conditioning(cond.to(model.device), null.to(model.device), 0, group)
-    if cond.shape[0] == len(natoms):
+    B, N = len(natoms), sum(natoms)
+    cond, null = _shared_conditioning(model, texts, B, text_embeds, null_text_embeds, group)
+    if cond is not None:
         cond, null = cond[g0:g1], null[g0:g1]
     node_base = sum(natoms[:g0])
-    if init is None:  # global initial noise from one seeded CPU generator, sliced per rank
-        g = torch.Generator().manual_seed(seed)
-        l0 = torch.randn(len(natoms), 3, 3, generator=g) * model.mask_lattice_matrix
-        x0 = torch.randn(sum(natoms), 3, generator=g)
-    else:
-        l0, x0 = init
     local = natoms[g0:g1]
+    n1 = node_base + sum(local)
+    if init is None and noise == "philox":  # global initial noise from one seeded CPU generator
+        g = torch.Generator().manual_seed(seed)
+        l0 = torch.randn(B, 3, 3, generator=g) * model.mask_lattice_matrix
+        x0 = torch.randn(N, 3, generator=g)
+        init = (l0, x0)
+    if init is not None:
+        l0, x0 = init
+        if l0.shape[0] != B or x0.shape[0] != N:
+            raise ValueError("init holds the global (l_T [B,3,3], x_T [N,3]) of the whole batch")
+        init = (l0[g0:g1], x0[node_base:n1])
+    natoms_all = [natoms[r0:r1] for r0, r1 in ranges]
+    it = model.sample_states(local, None, cond_scale, step_lr, noise=noise, seed=seed, text_embeds=cond,
+                             null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
+                             global_sizes=(N, B) if noise == "torch" else None, graph=graph)
+    want = None if isinstance(every_step, bool) else {int(t) for t in every_step}
+    for t, a, x, lat in it:
+        if t == 0 or (every_step is True) or (want is not None and t in want):
+            A_, X_, L_, _ = gather_states((a, x, lat), local, group, natoms_all=natoms_all)
+            yield t, A_, X_, L_
+
+
+@torch.no_grad()
+def sample_distributed(model, natoms: Sequence[int], cond: torch.Tensor, null: torch.Tensor, cond_scale=2.0,
+                       step_lr=1e-5, seed: int = 0, group=None, init: Optional[Tuple] = None, noise: str = "torch",
+                       graph: Optional[bool] = None):
+    """Sample `natoms` (global list) across all ranks; returns the global final
+    state (atom_types, frac_coords, lattices, natoms) on every rank.
+    `cond` / `null` are the [1 or B, text_dim] conditioning vectors held by
+    rank 0 (broadcast here). noise as in sample_states_distributed."""
     last = None
-    for last in model.sample_states(local, None, cond_scale, step_lr, noise="philox", seed=seed, text_embeds=cond,
-                                    null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0,
-                                    init=(l0[g0:g1], x0[node_base:node_base + sum(local)])):
+    for last in sample_states_distributed(model, natoms, None, cond_scale, step_lr, noise=noise, seed=seed,
+                                          text_embeds=cond, null_text_embeds=null, group=group, init=init,
+                                          graph=graph):
         pass
-    return gather_states(last[1:], local, group, natoms_all=[natoms[r0:r1] for r0, r1 in ranges])
+    _, a, x, lat = last
+    return a, x, lat, [int(n) for n in natoms]

@@ -44,6 +44,7 @@ from chemeleon_amd import _lib
 from chemeleon_amd.config import default_config
 from chemeleon_amd.modules.cspnet import CSPNet, SinusoidalTimeEmbeddings
 from chemeleon_amd.modules.schema import TrajectoryContainer, TrajectoryStep, step_to_atoms
+from chemeleon_amd.noise import StepNoise
 from chemeleon_amd.utils.diff_utils import D3PM, BetaScheduler, SigmaScheduler
 
 CHECKPOINT_DIR = os.environ.get("CHEMELEON_CHECKPOINT_DIR",
@@ -310,7 +311,8 @@ class Chemeleon(nn.Module):
                       text_embeds=None, null_text_embeds=None, clone: bool = True, t_stop: int = 0,
                       node_base: int = 0, graph_base: int = 0,
                       init: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-                      graph: Optional[bool] = None, lanes: int = 1) -> Iterator[Tuple]:
+                      graph: Optional[bool] = None, lanes: int = 1,
+                      global_sizes: Optional[Tuple[int, int]] = None) -> Iterator[Tuple]:
         """Reverse loop of chemeleon.py:305-467 yielding device tensors
         (t, atom_types [N], frac_coords [N,3] in [0,1), lattices [B,3,3]),
         starting with the pure-noise state at t = T.
@@ -326,7 +328,15 @@ class Chemeleon(nn.Module):
 
         Initial noise: from `init` = (l_T [B,3,3], x_T [N,3]) if given, else drawn
         on the CPU from the global generator (noise="torch", chemeleon.py:348-349)
-        or from Generator(seed) (noise="philox") for THIS batch. The per-step
+        or from Generator(seed) (noise="philox") for THIS batch.
+
+        global_sizes = (N_total, B_total) (noise="torch"): this batch is the shard
+        of a larger run whose crystals start at node_base / graph_base. Every
+        draw of the reference's stream (initial l_T, x_T; per step rand(N, A),
+        randn(B, 3, 3), randn(N, 3) x2) is then made at the GLOBAL size on the
+        CPU generator and this shard keeps its rows (chemeleon_amd.noise), so a
+        sample-parallel run reproduces the single-process trajectory bit for bit
+        and every rank's generator ends where the single-process one does. The per-step
         Philox noise is keyed by global node / graph index (node_base,
         graph_base), so a shard reproduces its crystals of a larger run exactly
         when it is also given that run's initial noise for them (init=, as
@@ -358,12 +368,22 @@ class Chemeleon(nn.Module):
             raise RuntimeError("Chemeleon (chemeleon_amd) samples on a HIP device only; call .to('cuda') first")
         B, N, A, T = len(natoms), sum(natoms), self.max_atoms, self.num_timesteps
         mask = self.mask_lattice_matrix
+        if global_sizes is None:
+            step_noise = StepNoise(N, B, A)
+        else:
+            if noise != "torch":
+                raise ValueError("global_sizes shards the reference's CPU RNG stream: it needs noise='torch'")
+            NG, BG = (int(v) for v in global_sizes)
+            if not (0 <= node_base and node_base + N <= NG and 0 <= graph_base and graph_base + B <= BG):
+                raise ValueError(f"shard nodes [{node_base}, {node_base + N}) / crystals [{graph_base}, "
+                                 f"{graph_base + B}) outside the global batch ({NG} nodes, {BG} crystals)")
+            step_noise = StepNoise(NG, BG, A, node_base, node_base + N, graph_base, graph_base + B)
         a = torch.zeros(N, dtype=torch.long, device=dev)  # chemeleon.py:347 (absorbing class 0)
         if init is not None:
             l0, x0 = init
         elif noise == "torch":
-            l0 = torch.randn(B, 3, 3) * mask  # :348
-            x0 = torch.randn(N, 3)  # :349
+            l0 = torch.randn(step_noise.B, 3, 3)[step_noise.g0:step_noise.g1] * mask  # :348
+            x0 = torch.randn(step_noise.N, 3)[step_noise.n0:step_noise.n1]  # :349
         else:
             g = torch.Generator().manual_seed(seed)
             l0 = torch.randn(B, 3, 3, generator=g) * mask
@@ -382,7 +402,7 @@ class Chemeleon(nn.Module):
         if graph and noise == "torch":
             if lanes > 1:
                 raise ValueError("lanes > 1 needs noise='philox'")
-            yield from self._replay_torch_noise(batch, sched, a, x, lat, cond, null, cond_scale, N, B, A, T, t_stop,
+            yield from self._replay_torch_noise(batch, sched, a, x, lat, cond, null, cond_scale, step_noise, T, t_stop,
                                                 emit)
             return
         if graph:
@@ -424,12 +444,8 @@ class Chemeleon(nn.Module):
                 yield (t - 1,) + emit(a, x, lat)
             return
         for t in range(T, t_stop, -1):
-            if noise == "torch" and t > 1:
-                ra = torch.rand((N, A)).to(dev, non_blocking=False)  # :400-404
-                rl = torch.randn(B, 3, 3).to(dev)  # :418
-                rx1 = torch.randn(N, 3).to(dev)  # :435
-                rx2 = torch.randn(N, 3).to(dev)  # :455
-                nz = (ra, rl, rx1, rx2)
+            if noise == "torch" and t > 1:  # :400-404, 418, 435, 455
+                nz = tuple(z.to(dev) for z in step_noise.draw())
             else:
                 nz = (None, None, None, None)
             _lib.check(L.chm_sample_step(batch.handle, sched, t, float(cond_scale), _lib.ptr(a), _lib.ptr(x),
@@ -437,12 +453,13 @@ class Chemeleon(nn.Module):
                                          seed, node_base, graph_base, stream), "chm_sample_step")
             yield (t - 1,) + emit(a, x, lat)
 
-    def _replay_torch_noise(self, batch, sched, a, x, lat, cond, null, cond_scale, N, B, A, T, t_stop, emit):
-        """Parity-mode noise (the reference's CPU RNG stream) under one captured reverse step."""
+    def _replay_torch_noise(self, batch, sched, a, x, lat, cond, null, cond_scale, step_noise, T, t_stop, emit):
+        """Parity-mode noise (the reference's CPU RNG stream, this shard's rows of it) under one captured
+        reverse step."""
         dev = self.device
         L = _lib.load()
         d_t = torch.full((1,), T, dtype=torch.int32, device=dev)
-        shapes = ((N, A), (B, 3, 3), (N, 3), (N, 3))
+        shapes = step_noise.local_shapes
         dnz = [torch.zeros(sh, dtype=torch.float32, device=dev) for sh in shapes]
         pin = [[torch.empty(sh, dtype=torch.float32).pin_memory() for sh in shapes] for _ in range(2)]
         done = [None, None]  # event after the last copy out of each pinned set
@@ -463,10 +480,7 @@ class Chemeleon(nn.Module):
                 k = t & 1
                 if done[k] is not None:
                     done[k].synchronize()  # the copy of two steps ago has left this pinned set
-                torch.rand(shapes[0], out=pin[k][0])
-                torch.randn(shapes[1], out=pin[k][1])
-                torch.randn(shapes[2], out=pin[k][2])
-                torch.randn(shapes[3], out=pin[k][3])
+                step_noise.draw(out=pin[k])
                 for dz, pz in zip(dnz, pin[k]):
                     dz.copy_(pz, non_blocking=True)
                 done[k] = torch.cuda.Event()
@@ -500,33 +514,70 @@ class Chemeleon(nn.Module):
                    "chm_sample_step")
         return a, x, lat
 
+    @staticmethod
+    def _distributed(distributed: Optional[bool], group) -> bool:
+        """Whether sample() / _sample_generator() shard over the ranks of `group`: `distributed` if
+        given, else whenever torch.distributed is initialised with more than one rank."""
+        if distributed is not None:
+            return bool(distributed)
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
     @torch.no_grad()
     def _sample_generator(self, natoms: Union[int, List[int]], texts: Optional[Union[str, List[str]]] = None,
-                          cond_scale: float = 2.0, step_lr: float = 1e-5, **kw):
+                          cond_scale: float = 2.0, step_lr: float = 1e-5, *, distributed: Optional[bool] = None,
+                          group=None, **kw):
         """chemeleon.py:305-467: yields, for every step t -> t-1, the list of
-        structures at t-1 (TrajectoryContainer.get_atoms, schema.py:57-83)."""
+        structures at t-1 (TrajectoryContainer.get_atoms, schema.py:57-83).
+        Under torch.distributed (see sample) the crystals are sharded over
+        the ranks and every step's whole batch is all-gathered to every rank."""
         if isinstance(natoms, int):
             natoms = [natoms]
-        it = self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw)
+        if texts is not None and isinstance(texts, str):
+            texts = [texts]
+        if self._distributed(distributed, group):
+            from chemeleon_amd.distributed import sample_states_distributed
+            it = sample_states_distributed(self, natoms, texts, cond_scale, step_lr, group=group, every_step=True,
+                                           **kw)
+        else:
+            it = self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw)
         next(it)
         for t, a, x, lat in it:
             yield step_to_atoms(a, x, lat, natoms)
 
     def sample(self, text_input: str, n_atoms: int, n_samples: int, cond_scale: float = 2.0, step_lr: float = 1e-5,
-               return_trajectory: bool = False, stream: bool = False, **kw):
+               return_trajectory: bool = False, stream: bool = False, *, distributed: Optional[bool] = None,
+               group=None, **kw):
         """chemeleon.py:469-490. Without return_trajectory / stream, only the
         final state is copied to the host (the reference converts every step).
         Keyword arguments go to sample_states: noise="philox" (device noise)
         or the default noise="torch" (the reference's CPU RNG stream); either
-        way one captured HIP graph is replayed per timestep (fc edges)."""
+        way one captured HIP graph is replayed per timestep (fc edges).
+
+        Multi-GPU: with torch.distributed initialised over more than one rank
+        (one process per GPU; or distributed=True / group=...), every rank
+        calls sample() with the same arguments and the same seeded generator;
+        the crystals are split over the ranks (chemeleon_amd.distributed), the
+        text conditioning is computed on rank 0 and broadcast, and every rank
+        returns the whole batch. In the default noise="torch" mode the result
+        is bit-identical to the single-process call. Only the final state is
+        exchanged, unless stream / return_trajectory ask for every step.
+        distributed=False keeps each rank's call local."""
         natoms = [n_atoms] * n_samples
         texts = [text_input] * n_samples if text_input is not None else None
+        kw.update(distributed=distributed, group=group)
         if stream:
             return self._sample_generator(natoms, texts, cond_scale, step_lr, **kw)
         if return_trajectory:
             return list(self._sample_generator(natoms, texts, cond_scale, step_lr, **kw))
+        kw.pop("distributed"), kw.pop("group")
+        if self._distributed(distributed, group):
+            from chemeleon_amd.distributed import sample_states_distributed
+            it = sample_states_distributed(self, natoms, texts, cond_scale, step_lr, group=group, **kw)
+        else:
+            it = self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw)
         last = None
-        for last in self.sample_states(natoms, texts, cond_scale, step_lr, clone=False, **kw):
+        for last in it:
             pass
         _, a, x, lat = last
         return step_to_atoms(a, x, lat, natoms)

@@ -83,8 +83,12 @@ void chm_model_destroy(chm_model* m);
 /* Launch-schedule options (not thread-safe against concurrent steps of the same model):
  *   "edge_split" (0 / 1): when edge layer 1's 256x256 tiles leave a partial last round of the
  *     grid, run that round in one grid with the edge-layer-2 tiles that do not read its rows.
- *   "edge16" (1 / 0): split16 edge GEMMs on v_mfma_f32_16x16x32_f16 (k_edge16, default) or on the
- *     round-1 32x32x16 kernels (k_edge_gemm); same arithmetic up to the MFMA's summation order.
+ *   "edge16" (1): accepted for compatibility (the round-1 32x32x16 kernels were removed; 0 fails).
+ *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag": edge-layer schedules
+ *     (bit-identical). The persistent one-grid kernel (edge_layer_dyn) runs only where
+ *     model creation saw 8 XCDs ("xcd_mask" = 0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD
+ *     exit, the launch's self-check must raise the repair), "edge_layer_repair", "edge_tail_timeout",
+ *     "edge_tail_norepair" (WRONG results after a timeout), "edge_rows_nowait".
  * Returns CHM_E_ARG for an unknown key. */
 int chm_model_set_option(chm_model* m, const char* key, int64_t value);
 
@@ -330,6 +334,8 @@ int chm_prof_read(int kernel, int64_t* launches, double* total_ms);
  *   out[CHM_EV_LAYER_REPAIR]   k_edge16_layer launches recomputed by their repair pair
  *   out[CHM_EV_TAIL_TIMEOUT]   k_edge16_tail: segment tiles whose wait for this grid's layer-1 tiles timed out
  *   out[CHM_EV_TAIL_REPAIR]    k_edge16_tail launches whose edge layer 2 was recomputed
+ *   out[CHM_EV_LAYER_INCOMPLETE] k_edge16_layer_dyn launches that ended with layer-2 tiles not computed (an
+ *                              XCD missing: the persistent kernel's static rows assume 8 XCDs; repaired)
  * Results never depend on these (a raised check is repaired before the layer's output is used); a
  * non-zero count means the run paid for the repairs. n <= 8 values are written. */
 #define CHM_EV_LAYER_TIMEOUT 0
@@ -337,8 +343,18 @@ int chm_prof_read(int kernel, int64_t* launches, double* total_ms);
 #define CHM_EV_LAYER_REPAIR 2
 #define CHM_EV_TAIL_TIMEOUT 3
 #define CHM_EV_TAIL_REPAIR 4
+#define CHM_EV_LAYER_INCOMPLETE 5
 int chm_prof_events(int64_t* out, int n);
 int chm_prof_events_reset(void);
+
+/* Host-only (no device): parity-mode atom-type noise for a shard of a sample-parallel run. Continues
+ * the MT19937 stream of the CPU torch generator (state[624], left, next as in ATen's
+ * mt19937_engine, i.e. the words of torch.Generator.get_state()) over `count` float uniforms, the
+ * stream torch.rand(count) draws (chemeleon.py:400-404: one 32-bit output y per element,
+ * (y & (2^24 - 1)) * 2^-24), and writes only elements [lo, hi) to out[hi - lo]. state / left / next
+ * are advanced in place. Replaces, per rank: torch.rand(N, A)[rows of this shard]. */
+int chm_mt19937_uniform(uint32_t* state, int32_t* left, int32_t* next, int64_t count, int64_t lo, int64_t hi,
+                        float* out);
 
 /* Sizes of the batch (for callers that allocate outputs). */
 int64_t chm_batch_num_nodes(const chm_batch* b);

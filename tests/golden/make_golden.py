@@ -334,6 +334,50 @@ def gen_large_steps(chm, csp):
         save(f"step_{tag}.npz", **rec)
 
 
+def gen_t1_logits(chm, csp):
+    """The reference's own CFG-mixed atom-type logits at t = 1 for the at-size step fixtures (VERDICT r3:
+    pin the t = 1 near-tie gate to reference data). At t = 1 the new types are the argmax of the
+    predictor's mixed logits (chemeleon.py:400-410, diff_utils.py:318-328); the predictor's
+    model_predictions output is recorded while the unmodified reference runs the same t = 1 step as
+    gen_large_steps. The step's outputs must equal the stored ones (same reference, same inputs), and
+    per atom the top-2 classes, the top-2 gap and the row's max |logit| are added to the fixture."""
+    T = 1000
+    m, sd = build_reference_model(chm, csp, T)
+    only = os.environ.get("CHM_GOLDEN_TAGS")
+    orig_mp = m.model_predictions
+    for tag, ts in LARGE_STEPS:
+        if 1 not in ts or (only and tag not in only.split(",")):
+            continue
+        path = os.path.join(HERE, f"step_{tag}.npz")
+        rec = dict(np.load(path))
+        natoms = rec["natoms"].tolist()
+        calls = []
+
+        def mp(*args, **kw):
+            out = orig_mp(*args, **kw)
+            calls.append(out[0].detach().clone())
+            return out
+
+        m.model_predictions = mp
+        try:
+            a = torch.from_numpy(rec["t1_a"].astype(np.int64))
+            nxt = reference_single_step(m, natoms, a, torch.from_numpy(rec["t1_x"]), torch.from_numpy(rec["t1_l"]), 1,
+                                        noise_seed=6000 + 1)
+        finally:
+            m.model_predictions = orig_mp
+        assert np.array_equal(nxt[0].numpy(), rec["t1_a_out"].astype(np.int64)), f"{tag}: types differ from the fixture"
+        assert np.array_equal(nxt[1].numpy(), rec["t1_x_out"]) and np.array_equal(nxt[2].numpy(), rec["t1_l_out"]), tag
+        mixed = calls[0]  # the predictor's mixed logits; the corrector call (calls[1]) does not set types
+        assert torch.equal(mixed.argmax(-1), nxt[0]), f"{tag}: t = 1 types are not the argmax of the predictor logits"
+        top = torch.topk(mixed, 2, dim=-1)
+        rec["t1_ref_top2"] = top.indices.to(torch.uint8).numpy()
+        rec["t1_ref_gap"] = (top.values[:, 0] - top.values[:, 1]).numpy()
+        rec["t1_ref_scale"] = mixed.abs().max(dim=-1).values.numpy()
+        g = rec["t1_ref_gap"] / rec["t1_ref_scale"]
+        print(f"{tag}: smallest relative top-2 gaps at t = 1:", np.sort(g)[:4], "atoms", np.argsort(g)[:4])
+        save(f"step_{tag}.npz", **rec)
+
+
 def reference_single_step(m, natoms, a, x, lat, t, noise_seed):
     """Run the reference generator for exactly one step at time t from the
     given state. The loop iterator (`tqdm(range(T, 0, -1))`,
@@ -684,6 +728,8 @@ if __name__ == "__main__":
         gen_single_steps(chm, csp)
     if "steps_large" in which:
         gen_large_steps(chm, csp)
+    if "t1_logits" in which:
+        gen_t1_logits(chm, csp)
     if "trajectory" in which:
         gen_trajectory(chm, csp)
     if "keys" in which:

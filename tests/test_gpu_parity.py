@@ -252,11 +252,13 @@ def test_teacher_forced_steps_at_size(model1000, golden, cn, tag):
 def _t1_near_ties(model, g, nat, cn, flipped, ref_a):
     """At t = 1 the types are the argmax of the CFG-mixed logits (no Gumbel noise, chemeleon.py:418 /
     diff_utils.py:286), so two classes whose logits agree to fp32 rounding are a tie that any other
-    summation order may break the other way (512 x 40, atom 7124: top-2 gap 2.4e-6 on logits of 4.41 in
-    the reference's own arithmetic, a few ulps). Such a flip is accepted only for near-ties: at most 2
-    atoms, each with the device's own top-2 gap below 1e-5 of the atom's logit scale and the reference's
-    choice one of the two. Returns the note printed with the step."""
+    summation order may break the other way (512 x 40, atom 7124). Such a flip is accepted only for
+    near-ties pinned on the REFERENCE's own logits: the fixture holds, per atom, the top-2 classes, the
+    top-2 gap and the max |logit| of the reference's mixed logits at t = 1 (make_golden.py gen_t1_logits).
+    At most 2 atoms; for each, the reference's gap <= 1e-5 of its logit scale, the device's gap likewise,
+    and the device's class is the reference's second choice. Returns the note printed with the step."""
     assert len(flipped) <= 2, f"t=1: {len(flipped)} atom types differ"
+    assert "t1_ref_gap" in g, "fixture lacks the reference's t = 1 logits (make_golden.py t1_logits)"
     B = len(nat)
     nat_t = torch.tensor(nat)
     te = model.time_embed(torch.full((B,), 1, dtype=torch.long)).to(DEV)
@@ -271,10 +273,36 @@ def _t1_near_ties(model, g, nat, cn, flipped, ref_a):
         top = torch.topk(mixed[i], 2)
         gap = float(top.values[0] - top.values[1])
         scale = float(mixed[i].abs().max())
-        assert gap <= 1e-5 * scale and int(ref_a[i]) in top.indices.tolist(), \
-            f"t=1 atom {i}: not a near-tie (top-2 gap {gap:.2e} of scale {scale:.2f}, reference class {int(ref_a[i])})"
-        notes.append(f"atom {i} gap {gap:.1e}")
+        rgap, rscale = float(g["t1_ref_gap"][i]), float(g["t1_ref_scale"][i])
+        rtop = [int(c) for c in g["t1_ref_top2"][i]]
+        assert rtop[0] == int(ref_a[i])
+        assert rgap <= 1e-5 * rscale, \
+            f"t=1 atom {i}: the reference's top-2 gap {rgap:.2e} (scale {rscale:.2f}) is no near-tie"
+        assert gap <= 1e-5 * scale, f"t=1 atom {i}: device top-2 gap {gap:.2e} of scale {scale:.2f}"
+        assert top.indices.tolist() == rtop[::-1], \
+            f"t=1 atom {i}: device top-2 {top.indices.tolist()} is not the reference's {rtop} swapped"
+        notes.append(f"atom {i} reference gap {rgap:.1e} (scale {rscale:.2f}), device gap {gap:.1e}")
     return "; near-tie flips: " + ", ".join(notes)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("math", ["split16", "f32"])
+def test_t1_step_512x40_math(model1000, golden, cn, math):
+    """configs[3] as one batch, t = 1 (the argmax step) in the shipped split16 arithmetic and in exact
+    fp32 MFMA arithmetic: which atoms' types differ from the reference (printed), under the gate of
+    _t1_near_ties."""
+    model1000.decoder.set_math(math)
+    g = golden("step_512x40.npz")
+    nat = g["natoms"].tolist()
+    a, x, lat = model1000.reverse_step(1, torch.from_numpy(g["t1_a"].astype(np.int64)), torch.from_numpy(g["t1_x"]),
+                                       torch.from_numpy(g["t1_l"]), nat, 2.0, 1e-5, cn[0], cn[1], noise=None)
+    ref_a = g["t1_a_out"].astype(np.int64)
+    flipped = np.nonzero(a.cpu().numpy() != ref_a)[0]
+    note = _t1_near_ties(model1000, g, nat, cn, flipped, ref_a) if len(flipped) else ""
+    rg = g["t1_ref_gap"] / g["t1_ref_scale"]
+    print(f"512x40 t=1 {math}: {len(flipped)} of {len(ref_a)} atom types differ from the reference "
+          f"(atoms {flipped.tolist()}){note}; the reference's smallest relative top-2 gaps: "
+          f"{', '.join(f'atom {i} {rg[i]:.1e}' for i in np.argsort(rg)[:3])}")
 
 
 @pytest.mark.parametrize("nat", [[40] * 64, [50] * 40, [23, 7, 40, 1, 80] * 23])
@@ -389,6 +417,41 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
                     (10, "one grid, static map + forced repair")):
         for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
             assert torch.equal(u, v), f"{what}: {name} differ from node-aligned segment tiles"
+
+
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23])
+def test_persistent_edge_kernel_with_a_missing_xcd_is_repaired(cn, nat):
+    """k_edge16_layer_dyn hands each of the 8 XCDs static row tiles. On a device (or partition mode)
+    with fewer XCDs those rows would never run: the launch counts its finished layer-2 tiles, the last
+    block out raises the repair request when any are missing, and the repair launches recompute the
+    layer. Forced here by making the blocks on XCD 5 exit at once ('edge_dyn_skip_xcd'):
+    the step equals the static map's bit for bit and the device counters record the incomplete
+    launches and their repairs. Model creation also probes the XCDs and runs the persistent form only
+    where all 8 were seen ('xcd_mask')."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(14)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    outs, events = [], []
+    for dyn, skip in ((0, -1), (2, -1), (2, 5)):
+        model.decoder.set_option("edge_layer_dyn", dyn)
+        model.decoder.set_option("edge_dyn_skip_xcd", skip)
+        _lib.prof_events(reset=True)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+        torch.cuda.synchronize()
+        events.append(_lib.prof_events())
+    del model
+    torch.cuda.empty_cache()
+    print("events (static map, persistent, persistent without XCD 5):", events)
+    assert events[1]["layer_incomplete"] == 0 and events[1]["layer_repairs"] == 0
+    assert events[2]["layer_incomplete"] == 12 and events[2]["layer_repairs"] == 12  # 2 decoder pairs x 6 layers
+    for k in (1, 2):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: persistent kernel (variant {k}) differs from the static map"
 
 
 def test_one_grid_edge_layers_single_conditioning(cn):
@@ -517,16 +580,22 @@ def test_trajectory_64x20_1000_steps(model1000, golden, cn):
     its types bit-exact in every stored state, |dx| <= 1e-4 (periodic) and its lattice within 1e-4
     normwise (max abs error / max |entry| of that crystal's lattice, per state)."""
     g = golden("trajectory_64x20_T1000.npz")
-    ts = [int(t) for t in g["t"]]
-    want = set(ts)
-    nat = [20] * 64
+    want = set(int(t) for t in g["t"])
     torch.manual_seed(42)
     got = {}
-    for st in model1000.sample_states(nat, None, 2.0, 1e-5, noise="torch", text_embeds=cn[0],
+    for st in model1000.sample_states([20] * 64, None, 2.0, 1e-5, noise="torch", text_embeds=cn[0],
                                       null_text_embeds=cn[1], clone=False):
         if st[0] in want:
             got[st[0]] = [v.cpu().numpy().copy() for v in st[1:]]
-    assert sorted(got) == sorted(want)
+    gate_64x20(got, g)
+
+
+def gate_64x20(got, g, label="64x20 T=1000"):
+    """The reference gate of test_trajectory_64x20_1000_steps on {t: (atom_types, frac, lattices)} of
+    the stored timesteps (also used by the sample-parallel run, tests/test_gpu_distributed.py)."""
+    ts = [int(t) for t in g["t"]]
+    nat = [20] * 64
+    assert sorted(got) == sorted(ts)
     a = np.stack([got[t][0] for t in ts])
     x = np.stack([got[t][1] for t in ts])
     lat = np.stack([got[t][2] for t in ts])
@@ -540,7 +609,7 @@ def test_trajectory_64x20_1000_steps(model1000, golden, cn):
     dx = float(d[:, clean].max()) if clean.any() else 0.0
     nw = (np.abs(lat - rl).max(axis=(2, 3)) / np.maximum(np.abs(rl).max(axis=(2, 3)), 1e-30))  # [state, crystal]
     lnw = float(nw[:, clean].max()) if clean.any() else 0.0
-    print(f"64x20 T=1000: crystals with an atom-type flip {int(flip.sum())}/{B} (first stored flip at t: {first}); "
+    print(f"{label}: crystals with an atom-type flip {int(flip.sum())}/{B} (first stored flip at t: {first}); "
           f"clean crystals: max |dx| {dx:.2e}, lattice normwise {lnw:.2e}; all crystals: max |dx| {float(d.max()):.2e}")
     assert flip.sum() <= 2, f"atom-type flips in {int(flip.sum())} crystals: {first}"
     assert dx <= 1e-4, dx

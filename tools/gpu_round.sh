@@ -33,7 +33,7 @@ for step in "$@"; do
         --no-cpu-baseline $arg > $f 2> $f.err || { tail -n 30 $f.err; exit 1; }
       python tools/bench_summary.py $f ;;
     prof)
-      D=$PWD/$O/prof
+      D=$PWD/$O/prof_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
       mkdir -p $D
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D -o run --output-format csv -- \
         python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-api-legs --no-traffic $arg \
