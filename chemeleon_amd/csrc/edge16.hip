@@ -889,7 +889,7 @@ struct SeqJob { int kind; long row; int sub; };  // kind 1: layer 1 (sub = colum
 // i = D, D+1, ... of [layer 1 of row i (2 jobs), layer 2 of row i - D (2P)] (the static map's pattern,
 // unbounded). Measured and not kept: the pool rows' layer-1 tiles running ahead twice as fast (so
 // that a backlog of layer-2 tiles covers the last row's layer-1 + layer-2 chain at the end): 512x40
-// 59.2 -> 60.6 ms per step (profiles/r3/ab_runahead.txt).
+// 59.2 -> 60.6 ms per step (profiles/r3/ab/ab_ra64/, ab_ra512/).
 __host__ __device__ inline SeqJob seq_job(long k, int P, int D) {
   const long G = 2 + 2L * P;
   if (k < 2L * D) return SeqJob{1, k / 2, (int)(k % 2)};

@@ -25,7 +25,8 @@ __device__ __forceinline__ void main_step(const char* lds, const char* gsrc, int
                                           f32x4 (&acc)[4][4]) {
   // stage: 8 x 1 KB per wave into this group's half of the LDS, ring of 2 (no reader of it: traffic only)
   char* ring = (char*)lds + (wave >> 2) * (64 * 1024) + (step & 1) * 32 * 1024 + (wave & 3) * 8 * 1024;
-  const char* src = gsrc + ((long)(blockIdx.x * 8 + wave) * 64 + (step & 63)) * 8192 + lane * 16;
+  // (an L2-resident source: 1 MB per XCD, as the edge kernels' W stream and re-read A rows)
+  const char* src = gsrc + ((long)((blockIdx.x & 15) * 8 + wave) * 8 + (step & 7)) * 8192 + lane * 16;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
     __builtin_amdgcn_global_load_lds((gbl_void*)(src + q * 1024), (lds_void*)(ring + q * 1024), 16, 0, 0);
@@ -51,6 +52,59 @@ __device__ __forceinline__ void main_step(const char* lds, const char* gsrc, int
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j][0], fa[i][0], acc[i][j], 0, 0, 0);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// Software-pipelined form (as the edge kernels): the fragments of step s were read during step s-1;
+// half of the MFMAs, the step's barrier (supplied by the caller between the halves: `mid`), then the
+// other half with the next step's 16 fragment reads spread between them (one read per MFMA pair
+// slot, sched_group_barrier).
+template <class Mid>
+__device__ __forceinline__ void main_step_pipe(const char* lds, const char* gsrc, int lane, int wave, int step,
+                                               f32x4 (&acc)[4][4], f16x8 (&fa)[2][4][2], f16x8 (&fw)[2][4][2],
+                                               int cur, Mid&& mid) {
+  char* ring = (char*)lds + (wave >> 2) * (64 * 1024) + (step & 1) * 32 * 1024 + (wave & 3) * 8 * 1024;
+  const char* src = gsrc + ((long)((blockIdx.x & 15) * 8 + wave) * 8 + (step & 7)) * 8192 + lane * 16;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    __builtin_amdgcn_global_load_lds((gbl_void*)(src + q * 1024), (lds_void*)(ring + q * 1024), 16, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[cur][j][1], fa[cur][i][0], acc[i][j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[cur][j][0], fa[cur][i][1], acc[i][j], 0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  mid();
+  const char* fr = lds + (wave >> 2) * (64 * 1024) + ((step + 1) & 1) * 32 * 1024 + lane * 16;
+  const int nx = cur ^ 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      fa[nx][i][p] = *reinterpret_cast<const f16x8*>(fr + (i * 2 + p) * 1024);
+      fw[nx][i][p] = *reinterpret_cast<const f16x8*>(fr + 8192 + (i * 2 + p) * 1024);
+    }
+#pragma unroll
+  for (int j = 2; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[cur][j][0], fa[cur][i][1], acc[i][j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[cur][j][0], fa[cur][i][0], acc[i][j], 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): next step's fragments are in
 }
 
 template <int E>
@@ -92,13 +146,39 @@ __global__ __launch_bounds__(512, 1) void k_probe(const char* gsrc, _Float16* gd
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.01f * i, 0.02f * j, 0.f, 1.f};
   float mx = 0.f;
-  const bool do_main = MODE == 0 || (grp == 0 && MODE != 3);
-  const bool do_epi = grp == 1 && (MODE == 1 || MODE == 3);
+  const int mode = MODE & 3;
+  const bool do_main = mode == 0 || (grp == 0 && mode != 3);
+  const bool do_epi = grp == 1 && (mode == 1 || mode == 3);
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-  for (int s = 0; s < steps; ++s) {
-    if (do_main) main_step(lds, gsrc, lane, wave, s, acc);
-    if (do_epi) epi_step<E>(lds, gdst, lane, wave, s, mx, acc);
-    __builtin_amdgcn_s_barrier();
+  if constexpr ((MODE & 4) == 0) {
+    for (int s = 0; s < steps; ++s) {
+      if (do_main) main_step(lds, gsrc, lane, wave, s, acc);
+      if (do_epi) epi_step<E>(lds, gdst, lane, wave, s, mx, acc);
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {  // pipelined main loop; the epilogue group does its step before the shared barrier
+    f16x8 fa[2][4][2], fw[2][4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        fa[0][i][p] = *reinterpret_cast<const f16x8*>(lds + lane * 16 + (i * 2 + p) * 1024);
+        fw[0][i][p] = *reinterpret_cast<const f16x8*>(lds + lane * 16 + 8192 + (i * 2 + p) * 1024);
+        fa[1][i][p] = fa[0][i][p];
+        fw[1][i][p] = fw[0][i][p];
+      }
+    auto bar = [] { __builtin_amdgcn_s_barrier(); };
+    for (int s = 0; s < steps; s += 2) {
+      if (do_main) {
+        main_step_pipe(lds, gsrc, lane, wave, s, acc, fa, fw, 0, bar);
+        main_step_pipe(lds, gsrc, lane, wave, s + 1, acc, fa, fw, 1, bar);
+      } else {
+        if (do_epi) epi_step<E>(lds, gdst, lane, wave, s, mx, acc);
+        __builtin_amdgcn_s_barrier();
+        if (do_epi) epi_step<E>(lds, gdst, lane, wave, s + 1, mx, acc);
+        __builtin_amdgcn_s_barrier();
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
@@ -150,7 +230,23 @@ int main(int argc, char** argv) {
   const double flops_main = 48.0 * 16 * 16 * 32 * 2;  // per wave per step
   printf("CUs %d, steps %d; per step per wave: 48 x 16x16x32 f16 MFMA (%.0f flop), 8 glds, 16 ds_read_b128\n", ncu,
          steps, flops_main);
-  for (int rep = 0; rep < 3; ++rep) {
+  for (int rep = 0; rep < 2; ++rep) {
+    double c;
+    double t0 = run<4, 8>(gsrc, gdst, sink, clk, blocks, steps, &c);
+    printf("PIPELINED mode 0 both groups main loop : %7.3f us/step  %6.0f TF/s (2 waves/SIMD)\n", t0,
+           flops_main * 8 * blocks / (t0 * 1e-6) / 1e12);
+    double t2 = run<6, 8>(gsrc, gdst, sink, clk, blocks, steps, &c);
+    printf("PIPELINED mode 2 main loop alone       : %7.3f us/step  %6.0f TF/s (1 wave/SIMD)\n", t2,
+           flops_main * 4 * blocks / (t2 * 1e-6) / 1e12);
+#define EPIP(E)                                                                                                    \
+  {                                                                                                                \
+    double t1 = run<5, E>(gsrc, gdst, sink, clk, blocks, steps, &c);                                              \
+    printf("PIPELINED E=%2d ping-pong %7.3f us/step = %.2f x main alone, %6.0f TF/s\n", E, t1, t1 / t2,            \
+           flops_main * 4 * blocks / (t1 * 1e-6) / 1e12);                                                         \
+  }
+    EPIP(4) EPIP(8) EPIP(12)
+  }
+  for (int rep = 0; rep < 1; ++rep) {
     double c;
     double t0 = run<0, 8>(gsrc, gdst, sink, clk, blocks, steps, &c);
     printf("mode 0 both groups main loop : %7.3f us/step  %6.0f TF/s (2 waves/SIMD)\n", t0,
