@@ -419,7 +419,7 @@ def main():
         dist.broadcast(null, 0)
 
     model.decoder.set_math(args.math)
-    draw_ms = None
+    draw_ms = draw_ms_8 = None
     if args.noise == "torch":
         # parity mode: every rank seeds the CPU generator alike and draws the whole job's tensors (initial
         # state and per-step noise), keeping its rows; the per-step host draw of this rank's share, timed alone
@@ -431,6 +431,15 @@ def main():
         for _ in range(10):
             sn.draw(out=bufs)
         draw_ms = (time.perf_counter() - t0) / 10 * 1e3
+        # and what one rank of an 8-rank run of this job draws per step (its rows of the global tensors)
+        r8 = partition(all_nat, 8)[0] if len(all_nat) >= 8 else (0, len(all_nat))
+        sn8 = StepNoise(sum(all_nat), total, A, 0, sum(all_nat[r8[0]:r8[1]]), r8[0], r8[1])
+        bufs8 = tuple(torch.empty(sh).pin_memory() for sh in sn8.local_shapes)
+        sn8.draw(out=bufs8)
+        t0 = time.perf_counter()
+        for _ in range(10):
+            sn8.draw(out=bufs8)
+        draw_ms_8 = (time.perf_counter() - t0) / 10 * 1e3
         torch.manual_seed(args.seed)
         it = model.sample_states(natoms, None, 2.0, 1e-5, noise="torch", text_embeds=cond, null_text_embeds=null,
                                  clone=False, node_base=node_base, graph_base=g0,
@@ -629,6 +638,7 @@ def main():
                  "edge_fourier_avg_ms": ms_fou / nfou if nfou else None,
                  "decoder_pair_avg_ms": ms_dec / ndec if ndec else None},
         "noise_host_draw_ms": draw_ms,
+        "noise_host_draw_ms_8rank_share": draw_ms_8,
         "edge_repairs": events["layer_repairs"] + events["tail_repairs"],
         "edge_events": dict(events, note="device counters over warm-up, timed and eager passes (chm_prof_events): "
                                          "repairs recompute a layer whose intra-grid check failed; 0 = none ran"),

@@ -36,6 +36,13 @@ struct GemmArgs {
   // of the output (after bias / activation / residual) is atomically max-ed into cmax[row] (float
   // bits as unsigned), for the next GEMM that reads C.
   const float* amax; const float* amax2; unsigned* cmax;
+  // split16 node GEMMs with PRE-SPLIT A (model option node_ps): A / A2 are then split rows [rows][K/16][hi 16 |
+  // lo 16] fp16 of A scaled per (row, 128-column chunk) by 2^-e, written by the kernel that produced A (no split
+  // inside the K loop: the register split was two thirds of the loop's VALU, PMC r4); aex / aex2 hold per row
+  // the 4 packed int8 exponents e of its 128-column chunks (A2's for the columns k >= ksplit); lda / lda2 in
+  // 4-byte units as for fp32 rows (one split row of K columns is K * 4 bytes). Cs / cex: the output C
+  // written the same way (the block's 128 columns are one chunk), besides or instead of the fp32 C.
+  const int* aex; const int* aex2; void* Cs; int* cex;
   // EPI_SEGMEAN (message GEMM + scatter_mean): row tiles cover whole nodes
   const int2* tiles; int ntiles;          // node ranges [x, y) of one conditioning
   const long* node_estart;                // first edge row of each node
@@ -72,6 +79,9 @@ struct EdgeArgs {
   const int* node_n;             // EPI_SEGMEAN: atom count of each node's crystal
   float* agg;
   unsigned* agg_max;             // EPI_SEGMEAN: max |agg[c][node][:]| atomically max-ed per row, or null
+  void* aggs; int* agge;         // EPI_SEGMEAN, pre-split node GEMMs: agg written as split rows [P*N][H/16][hi 16 |
+                                 // lo 16] scaled per 128-column chunk + the packed chunk exponents (agg then
+                                 // stays unwritten); null = fp32 agg
   // EPI_SEGMEAN on row tiles (k_edge16, fc batches): tile t = edge rows [256 t, 256 t + 256) of each
   // conditioning, nodes cut at tile ends (ntiles = row tiles). rtiles[t] = {first node starting in
   // the tile, first node starting after it, the node continued from tile t-1 or -1, its rows' offset
@@ -185,7 +195,9 @@ hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* 
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,
                         const int* natoms, long N, long E, int P, hipStream_t s);
 // rmax != null: rmax[row] = max |Hout[row, :]|
-hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr);
+// (Hs / He: also the rows split for the pre-split node GEMMs, GemmArgs::aex; film_ln's Hls / Hle likewise)
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr,
+                 void* Hs = nullptr, int* He = nullptr);
 // d_t != null: the time-embedding row is temb + (*d_t) * TD, shared by all graphs
 hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
                          int text_dim, float* cin, int B, int P, hipStream_t s);
@@ -199,7 +211,7 @@ hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldw
 enum { RMX_H = 0, RMX_HL = 1, RMX_AGG = 2, RMX_U = 3 };
 hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
                    const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s,
-                   float* rmx = nullptr, long rstride = 0);
+                   float* rmx = nullptr, long rstride = 0, void* Hls = nullptr, int* Hle = nullptr);
 hipError_t layer_norm(const float* X, float* Y, long rows, const float* w, const float* b, hipStream_t s);
 hipError_t graph_heads(const float* Hf, const float* Wlat, const float* lat, const int* node_off, const int* natoms,
                        long N, int B, int P, float* lat_out, hipStream_t s);

@@ -739,6 +739,30 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         f32x2e mean;
         mean.x = sacc.x / dv;
         mean.y = sacc.y / dv;
+        if (g.aggs) {
+          // pre-split node GEMMs: this wave's 128 columns are one chunk of the node MLP's A operand, written
+          // as a split row scaled by 2^-e (e from the chunk's max |agg|) with the chunk's exponent byte
+          float m = fmaxf(fabsf(mean.x), fabsf(mean.y));
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+          const int ex = exp_of(m);
+          const float sc = ldexpf(1.0f, -ex);
+          const float x0 = mean.x * sc, x1 = mean.y * sc;
+          typedef _Float16 f16x2s __attribute__((ext_vector_type(2)));
+          f16x2s hi, lo;
+          hi[0] = (_Float16)x0;
+          hi[1] = (_Float16)x1;
+          lo[0] = (_Float16)(x0 - (float)hi[0]);
+          lo[1] = (_Float16)(x1 - (float)hi[1]);
+          const long row = (long)seg_c * g.nnodes + node;
+          _Float16* o16 = reinterpret_cast<_Float16*>(g.aggs) + row * (2 * H) + (gcol >> 4) * 32 + (gcol & 15);
+          if (!(g.dbg & 4)) {
+            *reinterpret_cast<f16x2s*>(o16) = hi;
+            *reinterpret_cast<f16x2s*>(o16 + 16) = lo;
+            if (lane == 0) reinterpret_cast<signed char*>(g.agge)[row * 4 + (gcol >> 7)] = (signed char)ex;
+          }
+          return;
+        }
         if (!(g.dbg & 4)) *reinterpret_cast<f32x2e*>(g.agg + ((long)seg_c * g.nnodes + node) * H + gcol) = mean;
         if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it
           float m = fmaxf(fabsf(mean.x), fabsf(mean.y));
@@ -1037,10 +1061,10 @@ __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, 
                                                           long nrcnt = 0) {
   if (__hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   if (ev >= 0 && blockIdx.x == 0 && threadIdx.x == 0) count_event(ev);
-  if (EPI == EPI_EDGE && agg_max) {  // (and the row-tile flags, in case a wait timed out)
-    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
-    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrt; k += (long)gridDim.x * 512) lflags[k] = 0u;
-    for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrcnt; k += (long)gridDim.x * 512) rcnt[k] = 0u;
+  if (EPI == EPI_EDGE) {  // (and the row-tile flags, in case a wait timed out; null pointers come with 0 counts)
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; agg_max && k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; lflags && k < nrt; k += (long)gridDim.x * 512) lflags[k] = 0u;
+    for (long k = (long)blockIdx.x * 512 + threadIdx.x; rcnt && k < nrcnt; k += (long)gridDim.x * 512) rcnt[k] = 0u;
   }
   for (long vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     edge16_tile<EPI, ASC>(g, vb, nvb);

@@ -34,6 +34,47 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// A 512-column row held by one wave as 2 x float4 per lane (columns 4 lane .. +3 and 256 + 4 lane .. +3)
+// written as a split row for the pre-split node GEMMs (GemmArgs::aex): [H/16][hi 16 | lo 16] fp16 of the
+// row scaled by 2^-e per 128-column chunk (chunk = lanes 0-31 / 32-63 of v0, then of v1), e the exponent of
+// the chunk's max |value|; ex[row] = the 4 exponents as packed int8.
+typedef _Float16 f16x4k __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int exp_of_k(float m) {
+  int e = 0;
+  if (m > 0.f) frexpf(m, &e);
+  return e;
+}
+__device__ __forceinline__ void store_split_row512(const f32x4& v0, const f32x4& v1, int lane, void* rows, int* ex,
+                                                   long r) {
+  float m0 = fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w)));
+  float m1 = fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)));
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {  // within each half-wave: one 128-column chunk
+    m0 = fmaxf(m0, __shfl_xor(m0, o, 64));
+    m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
+  }
+  const int e0 = exp_of_k(m0), e1 = exp_of_k(m1);
+  _Float16* out = reinterpret_cast<_Float16*>(rows) + r * (2L * H);
+  const f32x4 vv[2] = {v0, v1};
+  const int ee[2] = {e0, e1};
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float sc = ldexpf(1.0f, -ee[p]);
+    const int col = 256 * p + 4 * lane;
+    f16x4k hi, lo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = vv[p][k] * sc;
+      hi[k] = (_Float16)x;
+      lo[k] = (_Float16)(x - (float)hi[k]);
+    }
+    *reinterpret_cast<f16x4k*>(out + (col >> 4) * 32 + (col & 15)) = hi;
+    *reinterpret_cast<f16x4k*>(out + (col >> 4) * 32 + 16 + (col & 15)) = lo;
+  }
+  const int e0b = __shfl(e0, 32, 64), e1b = __shfl(e1, 32, 64);
+  if (lane == 0) ex[r] = (e0 & 255) | ((e0b & 255) << 8) | ((e1 & 255) << 16) | ((e1b & 255) << 24);
+}
+
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (counter-based): perf-mode noise keyed by (seed, t, index)
 // ---------------------------------------------------------------------------
@@ -277,7 +318,8 @@ hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int*
 // ---------------------------------------------------------------------------
 // one wave per row (4 rows per block); rmax != null: the row's max |value| for the split16 node GEMMs
 __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, const float* __restrict__ emb,
-                                               float* __restrict__ Hout, long N, int P, float* __restrict__ rmax) {
+                                               float* __restrict__ Hout, long N, int P, float* __restrict__ rmax,
+                                               void* Hs, int* He) {
   const int lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N * P) return;
@@ -293,10 +335,12 @@ __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, co
     m = wave_max(m);
     if (lane == 0) rmax[r] = m;
   }
+  if (Hs) store_split_row512(v0, v1, lane, Hs, He, r);
 }
-hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax) {
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax, void* Hs,
+                 int* He) {
   const long rows = N * P;
-  hipLaunchKernelGGL(k_embed, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, emb, Hout, N, P, rmax);
+  hipLaunchKernelGGL(k_embed, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, emb, Hout, N, P, rmax, Hs, He);
   return hipGetLastError();
 }
 
@@ -374,7 +418,7 @@ __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, fl
                                                  float* __restrict__ Hl, const float* __restrict__ cond_emb,
                                                  const int* __restrict__ n2g, long N, int B, int P,
                                                  const float* fw, const float* fb, const float* lw, const float* lb,
-                                                 float* __restrict__ rmx, long rstride) {
+                                                 float* __restrict__ rmx, long rstride, void* Hls, int* Hle) {
   const int lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N * P) return;
@@ -405,6 +449,7 @@ __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, fl
   f32x4* l4 = reinterpret_cast<f32x4*>(Hl + r * H);
   l4[lane] = v0;
   l4[64 + lane] = v1;
+  if (Hls) store_split_row512(v0, v1, lane, Hls, Hle, r);
   if (rmx) {
     float m = 0.f;
 #pragma unroll
@@ -420,10 +465,10 @@ __global__ __launch_bounds__(256) void k_film_ln(const float* __restrict__ Y, fl
 }
 hipError_t film_ln(const float* Y, float* Hres, float* Hl, const float* cond_emb, const int* n2g, long N, int B, int P,
                    const float* fw, const float* fb, const float* lw, const float* lb, hipStream_t s, float* rmx,
-                   long rstride) {
+                   long rstride, void* Hls, int* Hle) {
   const long rows = N * P;
   hipLaunchKernelGGL(k_film_ln, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, Y, Hres, Hl, cond_emb, n2g, N, B,
-                     P, fw, fb, lw, lb, rmx, rstride);
+                     P, fw, fb, lw, lb, rmx, rstride, Hls, Hle);
   return hipGetLastError();
 }
 

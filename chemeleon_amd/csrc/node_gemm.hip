@@ -78,10 +78,94 @@ __device__ __forceinline__ void split3n(float x, __bf16& h, __bf16& m, __bf16& l
 
 }  // namespace
 
+// exponent e with m = f 2^e, f in [0.5, 1) (0 for m == 0): the split scale 2^-e keeps |x 2^-e| < 1
+__device__ __forceinline__ int exp_of_n(float m) {
+  int e = 0;
+  if (m > 0.f) frexpf(m, &e);
+  return e;
+}
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// The epilogue of a pre-split GEMM whose output feeds another one (GemmArgs::Cs): C (fp32, optional) and C
+// as split rows [rows][N/16][hi 16 | lo 16] scaled by 2^-e per (row, this block's 128 columns), e from the
+// row's max over the block's columns (the two column halves of a row sit in waves wn = 0 / 1: one LDS
+// exchange), with the packed exponent byte cex[row] byte n0 / 128.
+template <int NI, int NM>
+__device__ __forceinline__ void node_epilogue_split(const GemmArgs& g, f32x16 (&acc)[NI][2], const float (&aun)[NI],
+                                                    long row0, long nrows, int n0, int wm, int wn, int r32, int h) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* xm = reinterpret_cast<float*>(lds);  // [2 wm][2 wn][NM / 2 rows]
+  float cm[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const long lr = wm * (NM / 2) + i * 32 + r32;
+    const long row = row0 + (lr < nrows ? lr : nrows - 1);
+    const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+        v *= *reinterpret_cast<const f32x4*>(g.wscale + col) * aun[i];
+        if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+        if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+        if (g.act == 1)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
+        if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+        if (g.C && lr < nrows) *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] = v[e];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      }
+    cm[i] = fmaxf(m, __shfl_xor(m, 32, 64));  // lanes r32 and r32 + 32 hold the same row
+  }
+  __syncthreads();  // every wave is past its K loop: the stages are free
+  if (h == 0)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) xm[(wm * 2 + wn) * (NM / 2) + 32 * i + r32] = cm[i];
+  __syncthreads();
+  _Float16* Cs = reinterpret_cast<_Float16*>(g.Cs);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const long lr = wm * (NM / 2) + i * 32 + r32;
+    if (lr >= nrows) continue;
+    const long row = row0 + lr;
+    const int ex = exp_of_n(fmaxf(cm[i], xm[(wm * 2 + (wn ^ 1)) * (NM / 2) + 32 * i + r32]));
+    const float sc = ldexpf(1.0f, -ex);
+    _Float16* out = Cs + row * (2L * g.N);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gc = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;  // 16-column K-tile gc >> 4, offset gc & 15
+        f16x4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = acc[i][j][4 * q + e] * sc;
+          hi[e] = (_Float16)x;
+          lo[e] = (_Float16)(x - (float)hi[e]);
+        }
+        *reinterpret_cast<f16x4*>(out + (gc >> 4) * 32 + (gc & 15)) = hi;
+        *reinterpret_cast<f16x4*>(out + (gc >> 4) * 32 + 16 + (gc & 15)) = lo;
+      }
+    if (wn == 0 && h == 0) reinterpret_cast<signed char*>(g.cex)[row * 4 + n0 / 128] = (signed char)ex;
+  }
+}
+
 // VAR (microbenchmark only): 1 = A split replaced by one conversion (wrong results; VALU probe)
-template <int VAR, bool S16, int NB, int NMT = 128>
+// PS (S16 only): A arrives pre-split (GemmArgs::aex): its fragments are read from LDS as they are, the
+// accumulators are rescaled by 2^(e_prev - e_next) where a 128-column chunk of K ends (exact), and the
+// epilogue can write C split the same way (GemmArgs::Cs).
+template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4), "tiling");
+  static_assert(!PS || S16, "pre-split A is a split16 form");
   constexpr int NM = NMT, NI = NMT / 64;  // tile rows; 32-row fragment groups per wave
   constexpr int A_STB_ = A_STB<NMT>;
   // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
@@ -165,7 +249,22 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   float asc[NI], aun[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) asc[i] = aun[i] = 1.0f;
-  if constexpr (S16) {
+  // PS: this lane's rows' chunk exponents (chunks [0, nc1) from aex, the rest from aex2)
+  int pex[NI], pex2[NI];
+  const int nc1 = g.ksplit / 128;
+  auto chunk_e = [&](int i, int c) __attribute__((always_inline)) {
+    return c < nc1 ? (int)(signed char)(pex[i] >> (8 * c)) : (int)(signed char)(pex2[i] >> (8 * (c - nc1)));
+  };
+  if constexpr (PS) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int lr = wm * (NM / 2) + 32 * i + r32;
+      const long ar = row0 + (lr < nrows ? lr : nrows - 1);
+      pex[i] = g.aex[ar];
+      pex2[i] = g.aex2 ? g.aex2[ar] : 0;
+      aun[i] = ldexpf(1.0f, chunk_e(i, g.K / 128 - 1));  // (the last chunk's scale, undone in the epilogue)
+    }
+  } else if constexpr (S16) {
     if (g.amax) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -193,12 +292,19 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   typedef std::conditional_t<S16, f16x8, bf16x8> frag;
   f32x4 ra0[NI], ra1[NI];
   frag fa[2][NP][NI], fwt[2][NP][2];  // [set][part][i / j]
+  // PS: the A fragments as they are (hi piece h, lo piece 2 + h of the row's 64-B K-tile, swizzled like W16)
+  const int fa16[2] = {(wm * (NM / 2) + r32) * A_ROWB + 16 * (h ^ asw), (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 + h) ^ asw)};
   auto read_raw = [&](int t, int set) {
     const char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      ra0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
-      ra1[i] = *reinterpret_cast<const f32x4*>(st + fa1 + i * 32 * A_ROWB);
+      if constexpr (PS) {
+        fa[set][0][i] = *reinterpret_cast<const frag*>(st + fa16[0] + i * 32 * A_ROWB);
+        fa[set][1][i] = *reinterpret_cast<const frag*>(st + fa16[1] + i * 32 * A_ROWB);
+      } else {
+        ra0[i] = *reinterpret_cast<const f32x4*>(st + fa0 + i * 32 * A_ROWB);
+        ra1[i] = *reinterpret_cast<const f32x4*>(st + fa1 + i * 32 * A_ROWB);
+      }
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p)
@@ -208,6 +314,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
                              : *reinterpret_cast<const frag*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
   };
   auto split = [&](int set) {
+    if constexpr (PS) return;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       if constexpr (S16) {
@@ -262,6 +369,17 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   split(0);
   auto step = [&](int t, auto CUR) {
     constexpr int cur = decltype(CUR)::value;
+    if constexpr (PS) {  // tile t opens a new 128-column chunk of A: move the accumulators to its scale
+      if (t > 0 && (t & 7) == 0) {
+        const int c = t >> 3;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const float f = ldexpf(1.0f, chunk_e(i, c - 1) - chunk_e(i, c));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] *= f;
+        }
+      }
+    }
     // this thread's part of tile t+1 has landed (AHEAD - 2 tiles may stay in flight)
     vm_wait<(AHEAD - 2) * GL>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -312,6 +430,12 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 
   // lane l owns output row wm*NM/2 + 32i + (l & 31) and, per 4-register group q, the four
   // consecutive columns wn*64 + 32j + 8q + 4h .. +3
+  if constexpr (PS) {
+    if (g.Cs) {  // the output as split rows too: this block's 128 columns are one chunk of the next GEMM's A
+      node_epilogue_split<NI, NM>(g, acc, aun, row0, nrows, n0, wm, wn, r32, h);
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const long lr = wm * (NM / 2) + i * 32 + r32;
@@ -353,14 +477,17 @@ constexpr int LDS3 = STB<true> * NST<true, 3>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
 
 static hipError_t node_gemm_init_once() {
-  const void* ks[10] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
+  const void* ks[14] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
                         (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
                         (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
                         (const void*)k_node_gemm<0, true, 3, 64>, (const void*)k_node_gemm<1, true, 3, 64>,
-                        (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>};
-  const int bytes[10] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4};
+                        (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>,
+                        (const void*)k_node_gemm<0, true, 2, 128, true>, (const void*)k_node_gemm<0, true, 3, 128, true>,
+                        (const void*)k_node_gemm<0, true, 3, 64, true>, (const void*)k_node_gemm<0, true, 4, 64, true>};
+  const int bytes[14] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4,
+                         NODE_LDS, LDS3, LDS64_3, LDS64_4};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 10 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  for (int i = 0; i < 14 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
 
@@ -379,7 +506,8 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   static const int linear = getenv("CHM_NODE_LINEAR") ? atoi(getenv("CHM_NODE_LINEAR")) : 0;  // (A/B only)
   GemmArgs g = g_in;
   g.linear_order = linear;
-  if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || !g.C) return hipErrorInvalidValue;
+  if (g.M <= 0 || g.N % NN || g.K % (2 * NK) || g.ksplit % NK || !g.Wp3 || !g.A || (!g.C && !g.Cs))
+    return hipErrorInvalidValue;
   if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
   if (hipError_t e = node_gemm_init(); e != hipSuccess) return e;
   const long blocks = ((g.M + 127) / 128) * (g.N / NN);
@@ -389,6 +517,22 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   // 26 us at K = 512); above that 128-row tiles at three blocks per CU (M = 20480: 54 vs 65 us with
   // two), profiles/r2/node/node64_micro.log
   const int rows = g_node_rows ? g_node_rows : (blocks < 256 ? 64 : 128);
+  if (g.aex) {  // pre-split A (split16 only)
+    if (!g.wscale || g.K % 128 || g.ksplit % 128 || (g.Cs && (g.N % 128 || !g.cex))) return hipErrorInvalidValue;
+    const int nb = g_node_blocks ? g_node_blocks : 3;
+    if (rows == 64) {
+      const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
+      if (nb == 4)
+        hipLaunchKernelGGL((k_node_gemm<0, true, 4, 64, true>), grid64, block, LDS64_4, s, g);
+      else
+        hipLaunchKernelGGL((k_node_gemm<0, true, 3, 64, true>), grid64, block, LDS64_3, s, g);
+    } else if (nb == 3) {
+      hipLaunchKernelGGL((k_node_gemm<0, true, 3, 128, true>), grid, block, LDS3, s, g);
+    } else {
+      hipLaunchKernelGGL((k_node_gemm<0, true, 2, 128, true>), grid, block, NODE_LDS, s, g);
+    }
+    return hipGetLastError();
+  }
   if (g.wscale && rows == 64) {
     const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
     if (g_node_blocks == 4)

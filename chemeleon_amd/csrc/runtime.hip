@@ -73,6 +73,8 @@ struct chm_model {
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
+  int node_ps = 1;       // CHM_NODE_PS=0: split16 node GEMMs split their A operands in the K loop (r3) instead of
+                         // reading them pre-split from the producing kernels (r4)
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge16.hip)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
@@ -118,6 +120,11 @@ struct chm_batch {
   // workspace
   float *cin, *cemb, *Hres, *Hl, *Y, *agg, *PQ, *gbias, *F, *S, *M, *Hf, *HO, *LAT;
   float* rmx;        // split16 node GEMMs: the four row-max arrays [4][P*N] (RMX_*)
+  // split16 pre-split node GEMMs (node_ps): the node GEMMs' A operands as split rows [P*N][H/16][hi 16 | lo 16]
+  // fp16 + per row the packed int8 exponents of its four 128-column chunks: the residual stream (FiLM
+  // projection), the layer-normed rows (P / Q halves, node MLP 1), agg (node MLP 1), U (node MLP 2)
+  void *Hs, *Hls, *aggs, *Us;
+  int *He, *Hle, *agge, *Ue;
   unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
   void* owned = nullptr;  // the library's own allocation (chm_batch_create); null for caller workspaces
   size_t bytes = 0;
@@ -288,6 +295,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (ng) m->node_glds = atoi(ng);
     const char* n16 = getenv("CHM_NODE16");
     if (n16) m->node16 = atoi(n16);
+    const char* nps = getenv("CHM_NODE_PS");
+    if (nps) m->node_ps = atoi(nps);
     m->edge_trace = getenv("CHM_EDGE_TRACE");
     const char* tl = getenv("CHM_EDGE_TRACE_LAYER");
     if (tl) m->edge_trace_layer = atoi(tl);
@@ -406,6 +415,10 @@ extern "C" int chm_model_get_math(const chm_model* m) { return m ? m->math : -1;
 extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value) {
   if (!m || !key) return fail(CHM_E_ARG, "NULL argument");
   const std::string k = key;
+  if (k == "node_ps") {  // split16 node GEMMs read pre-split A operands (1) or split them in the K loop (0)
+    m->node_ps = value != 0;
+    return CHM_OK;
+  }
   if (k == "edge_split") {
     m->edge_split = value != 0;
     return CHM_OK;
@@ -718,6 +731,17 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
   b->rmx = fl((size_t)4 * P * N);
+  if (b->math == MATH_SPLIT16) {
+    void** sp[4] = {&b->Hs, &b->Hls, &b->aggs, &b->Us};
+    int** se[4] = {&b->He, &b->Hle, &b->agge, &b->Ue};
+    for (int k = 0; k < 4; ++k) {
+      *sp[k] = carve((size_t)P * N * H * 4);
+      *se[k] = (int*)carve((size_t)P * N * sizeof(int));
+    }
+  } else {
+    b->Hs = b->Hls = b->aggs = b->Us = nullptr;
+    b->He = b->Hle = b->agge = b->Ue = nullptr;
+  }
   b->tail_flags = (unsigned*)carve(kMaxTailTiles * sizeof(unsigned));
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
@@ -1012,7 +1036,7 @@ static GemmArgs gargs(long M, int N, int K, const float* A, long lda, const floa
 static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* W3, hipStream_t s,
                            const void* W16 = nullptr, const float* wsc = nullptr) {
   if (b->math == MATH_F32) return gemm(g, epi, s);
-  if (b->math == MATH_SPLIT16 && W16 && g.amax && b->m->node16 && b->m->node_glds && epi == EPI_STD) {
+  if (b->math == MATH_SPLIT16 && W16 && (g.amax || g.aex) && b->m->node16 && b->m->node_glds && epi == EPI_STD) {
     g.Wp3 = W16; g.wscale = wsc;
     return node_gemm(g, s);
   }
@@ -1123,15 +1147,17 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   ProfScope whole(CHM_K_DECODER, s);
   // split16 node GEMMs: row maxima of their A operands, written by the producing kernels
   const bool n16 = b->math == MATH_SPLIT16 && m->node16 && m->node_glds;
+  // pre-split node GEMMs: the producers write the A operands split (no row-max atomics then)
+  const bool ps = n16 && m->node_ps && b->Hs;
   const long RS = (long)b->P * N;
-  auto rmx = [&](int k) { return n16 ? b->rmx + k * RS : nullptr; };
+  auto rmx = [&](int k) { return n16 && !ps ? b->rmx + k * RS : nullptr; };
   if (m->film && !reuse_cond) {
     HIPCHK(build_cond_in(temb, tstride, d_t, text0, text1, X, b->cin, B, P, s));
     GemmArgs g = gargs((long)P * B, 2 * H, CIN, b->cin, CIN, m->Wc, b->cemb, 2 * H);
     g.bias = m->bc; g.act = 1;
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
-  HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H)));
+  HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H), ps ? b->Hs : nullptr, ps ? b->He : nullptr));
   if (b->math == MATH_SPLIT16)
     HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s, b->knn ? b->fd : nullptr));  // fp16 hi/lo split rows
   else
@@ -1157,21 +1183,27 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
     if (m->film) {  // FiLM projection (cspnet.py:92)
-      GemmArgs g = gargs(R, H, H, b->Hres, H, m->Wp, b->Y, H);
+      GemmArgs g = gargs(R, H, H, ps ? (const float*)b->Hs : b->Hres, H, m->Wp, b->Y, H);
       g.bias = m->bp; g.amax = rmx(RMX_H);
+      if (ps) g.aex = b->He;
       HIPCHK(run_gemm(b, g, EPI_STD, m->Wp3, s, m->Wp16, m->Wpsc));
     }
     // FiLM + residual + the layer's LayerNorm (film-less: the LayerNorm only)
     HIPCHK(film_ln(m->film ? b->Y : nullptr, b->Hres, b->Hl, b->cemb, b->n2g, N, B, P, m->fw, m->fb, w.lw, w.lb, s,
-                   rmx(0), RS));
+                   rmx(0), RS, ps ? b->Hls : nullptr, ps ? b->Hle : nullptr));
     {  // per-node halves of the first edge layer: [P | Q] = Hl [A ; Bm]^T, P += b1 + C vec(LL^T)
-      GemmArgs g = gargs(R, 2 * H, H, b->Hl, H, w.WAB, b->PQ, 2 * H);
+      GemmArgs g = gargs(R, 2 * H, H, ps ? (const float*)b->Hls : b->Hl, H, w.WAB, b->PQ, 2 * H);
       g.gb = b->gbias + (size_t)l * B * H; g.ldgb = H; g.gb_cols = H; g.row2g = b->n2g; g.gb_rowmod = N;
       g.amax = rmx(RMX_HL);
+      if (ps) g.aex = b->Hle;
       HIPCHK(run_gemm(b, g, EPI_STD, w.WAB3, s, w.WAB16, w.WABsc));
     }
     if (b->math == MATH_SPLIT16 && E == 0) {  // (knn: no atom within any other's radius: every mean is 0)
       HIPCHK(hipMemsetAsync(b->agg, 0, (size_t)P * N * H * sizeof(float), s));
+      if (ps) {
+        HIPCHK(hipMemsetAsync(b->aggs, 0, (size_t)P * N * H * 4, s));
+        HIPCHK(hipMemsetAsync(b->agge, 0, (size_t)P * N * sizeof(int), s));
+      }
     } else if (b->math == MATH_SPLIT16) {
       // split16: fp16 hi/lo split rows throughout (edge16.hip). S lives in S's bytes as
       // split rows [P*E][H/32][2][32] plus one packed exponent word per row (rowmax buffer).
@@ -1191,6 +1223,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       e2.ntiles = b->ntiles;
       e2.node_estart = b->node_estart; e2.natoms = b->natoms; e2.n2g = b->n2g; e2.agg = b->agg;
       e2.node_n = b->node_n; e2.agg_max = reinterpret_cast<unsigned*>(rmx(RMX_AGG));
+      if (ps) { e2.aggs = b->aggs; e2.agge = b->agge; }
       e2.nnodes = N; e2.npairs = P; e2.E = E; e2.dbg = m->edge_dbg; e2.stagger = m->edge_stagger;
       if (m->edge_rows && b->rtiles) {  // 256-row tiles, cut nodes continued across tiles
         e2.rtiles = b->rtiles; e2.ntiles = (int)b->nrt; e2.sbuf = b->sbuf; e2.msgbuf = b->msgbuf;
@@ -1274,12 +1307,20 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       GemmArgs g = gargs(R, H, 2 * H, b->Hl, H, w.W3, b->Y, H);
       g.A2 = b->agg; g.lda2 = H; g.ksplit = H; g.bias = w.b3; g.act = 1;
       g.amax = rmx(RMX_HL); g.amax2 = rmx(RMX_AGG); g.cmax = reinterpret_cast<unsigned*>(rmx(RMX_U));
+      if (ps) {  // U exists only as the next GEMM's split operand
+        g.A = (const float*)b->Hls; g.A2 = (const float*)b->aggs; g.aex = b->Hle; g.aex2 = b->agge;
+        g.C = nullptr; g.Cs = b->Us; g.cex = b->Ue;
+      }
       HIPCHK(run_gemm(b, g, EPI_STD, w.W33, s, w.W316, w.W3sc));
     }
     {  // node MLP 2 + residual: Hres += SiLU(U W4^T + b4)
       GemmArgs g = gargs(R, H, H, b->Y, H, w.W4, b->Hres, H);
       g.bias = w.b4; g.act = 1; g.R = b->Hres; g.ldr = H;
       g.amax = rmx(RMX_U); g.cmax = reinterpret_cast<unsigned*>(rmx(RMX_H));
+      if (ps) {  // (and the residual stream split for the next layer's FiLM projection)
+        g.A = (const float*)b->Us; g.aex = b->Ue;
+        if (l + 1 < L && m->film) { g.Cs = b->Hs; g.cex = b->He; }
+      }
       HIPCHK(run_gemm(b, g, EPI_STD, w.W43, s, w.W416, w.W4sc));
     }
   }

@@ -454,6 +454,42 @@ def test_persistent_edge_kernel_with_a_missing_xcd_is_repaired(cn, nat):
             assert torch.equal(u, v), f"{what}: persistent kernel (variant {k}) differs from the static map"
 
 
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23])
+def test_presplit_node_gemms_match_in_loop_split(cn, nat):
+    """split16 node GEMMs reading their A operands pre-split by the producing kernels (option 'node_ps', the
+    default: film_ln, embed, the segment-mean epilogue and the node GEMM epilogues write split rows scaled per
+    128-column chunk; the GEMM rescales its accumulators at chunk boundaries) against the in-loop register
+    split of round 3 (per-row scales): same types, coordinates and lattices to fp32-rounding level (the two
+    differ only in where the power-of-two scales change), and the decoder outputs within 8e-6 scaled (the
+    bound test_math_modes_agree puts between split16 and exact fp32)."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(15)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    te = model.time_embed(torch.full((B,), 300, dtype=torch.long)).to(DEV)
+    nat_t = torch.tensor(nat)
+    steps, decs = [], []
+    for ps in (1, 0):
+        model.decoder.set_option("node_ps", ps)
+        steps.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+        o = model.decoder(atom_types=a0.to(DEV), frac_coords=x0.to(DEV), lattices=l0.to(DEV), num_atoms=nat_t.to(DEV),
+                          node2graph=torch.arange(B).repeat_interleave(nat_t).to(DEV), t=te,
+                          text_embeds=cn[0].expand(B, -1).to(DEV))
+        decs.append([o.node_features.cpu(), o.atom_types_out.cpu(), o.coords_out.cpu(), o.lattice_out.cpu()])
+    del model
+    torch.cuda.empty_cache()
+    assert torch.equal(steps[0][0], steps[1][0]), "atom types differ between the two node-GEMM forms"
+    dx = periodic_close(steps[0][1], steps[1][1], tol=1e-5, what="frac")
+    dl = close(steps[0][2], steps[1][2], rtol=1e-5, what="lattice")
+    errs = [close(u, v, rtol=8e-6, what=w) for u, v, w in zip(decs[0], decs[1], ("node", "types", "coords", "lattice"))]
+    print(f"pre-split vs in-loop split: step |dx| {dx:.2e}, lattice {dl:.2e}; decoder scaled errors "
+          + ", ".join(f"{e:.1e}" for e in errs))
+
+
 def test_one_grid_edge_layers_single_conditioning(cn):
     """k_edge16_layer with one conditioning (P = 1: a plain decoder call, as the CrystalClip graph
     encoder and `CSPNet.forward` make): 64 x 40 (400 row tiles, above the one-grid threshold) and a
