@@ -73,13 +73,15 @@ struct chm_model {
   int edge_dbg = 0;      // CHM_EDGE_DBG: edge-GEMM ablations for profiling only (wrong results)
   int node_glds = 1;     // CHM_NODE_GLDS=0: node GEMMs on the register-staged k_gemm3 (bit-identical, 2-3% slower)
   int node16 = 1;        // CHM_NODE16=0: split16 mode keeps its node GEMMs on bf16x3
-  int node_ps = 1;       // CHM_NODE_PS=0: split16 node GEMMs split their A operands in the K loop (r3) instead of
-                         // reading them pre-split from the producing kernels (r4)
+  int node_ps = 0;       // CHM_NODE_PS=1: split16 node GEMMs read their A operands pre-split by the producing
+                         // kernels instead of splitting them in the K loop (r4; measured 0.5% slower per step,
+                         // DESIGN.md §4 "Node GEMMs")
   int edge_stagger = 0;  // CHM_EDGE_STAGGER: first-round start delay of every other CU (edge16.hip)
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
   int edge_lag = 10;     // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD
+  long edge_layer_min = kLayerMinTiles;  // CHM_EDGE_LAYER_MIN: row tiles from which the one-grid kernel runs
   int edge_dyn = 1;      // CHM_EDGE_DYN: one-grid kernel form, 0 static block -> job map (k_edge16_layer), 1 the
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
@@ -310,6 +312,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (lay) m->edge_layer = atoi(lay);
     const char* lag = getenv("CHM_EDGE_LAG");
     if (lag) m->edge_lag = atoi(lag) > 0 ? atoi(lag) : 1;
+    const char* lmin = getenv("CHM_EDGE_LAYER_MIN");
+    if (lmin) m->edge_layer_min = atol(lmin);
     const char* rg = getenv("CHM_REPAIR_GRID");
     if (rg) m->repair_grid = atoi(rg);
     const char* dyn = getenv("CHM_EDGE_DYN");
@@ -447,6 +451,11 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
   }
   if (k == "xcd_mask") {  // (tests) override the XCD mask probed at creation
     m->xcd_mask = (unsigned)value;
+    return CHM_OK;
+  }
+  if (k == "edge_layer_min") {  // row tiles from which both edge layers run in one grid (default 256)
+    if (value < 1) return fail(CHM_E_ARG, "edge_layer_min must be >= 1");
+    m->edge_layer_min = (long)value;
     return CHM_OK;
   }
   if (k == "edge_pool") {  // its run-time-claimed share of the row tiles, percent (0: static rows only)
@@ -1234,7 +1243,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (e2.rtiles && m->edge_layer && b->nrt >= kLayerMinTiles && (!m->edge_trace || m->edge_trace_layer == 3)) {
+      if (e2.rtiles && m->edge_layer && b->nrt >= m->edge_layer_min && (!m->edge_trace || m->edge_trace_layer == 3)) {
         // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
         e1.lflags = e2.lflags = b->lflags;
         e1.xbad = e2.xbad = b->xbad + l;

@@ -456,8 +456,9 @@ def test_persistent_edge_kernel_with_a_missing_xcd_is_repaired(cn, nat):
 
 @pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23])
 def test_presplit_node_gemms_match_in_loop_split(cn, nat):
-    """split16 node GEMMs reading their A operands pre-split by the producing kernels (option 'node_ps', the
-    default: film_ln, embed, the segment-mean epilogue and the node GEMM epilogues write split rows scaled per
+    """split16 node GEMMs reading their A operands pre-split by the producing kernels (option 'node_ps', off by
+    default since it measured no faster: film_ln, embed, the segment-mean epilogue and the node GEMM epilogues
+    write split rows scaled per
     128-column chunk; the GEMM rescales its accumulators at chunk boundaries) against the in-loop register
     split of round 3 (per-row scales): same types, coordinates and lattices to fp32-rounding level (the two
     differ only in where the power-of-two scales change), and the decoder outputs within 8e-6 scaled (the
