@@ -84,8 +84,10 @@ void chm_model_destroy(chm_model* m);
  *   "edge_split" (0 / 1): when edge layer 1's 256x256 tiles leave a partial last round of the
  *     grid, run that round in one grid with the edge-layer-2 tiles that do not read its rows.
  *   "edge16" (1): accepted for compatibility (the round-1 32x32x16 kernels were removed; 0 fails).
- *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag": edge-layer schedules
- *     (bit-identical). The persistent one-grid kernel (edge_layer_dyn) runs only where
+ *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag", "edge_layer_min": edge-layer
+ *     schedules (bit-identical).
+ *   "node_ps" (0 / 1): split16 node GEMMs read their A operands pre-split by the producing kernels (not
+ *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs"). The persistent one-grid kernel (edge_layer_dyn) runs only where
  *     model creation saw 8 XCDs ("xcd_mask" = 0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD
  *     exit, the launch's self-check must raise the repair), "edge_layer_repair", "edge_tail_timeout",
  *     "edge_tail_norepair" (WRONG results after a timeout), "edge_rows_nowait".

@@ -86,3 +86,79 @@ def test_two_rank_gather_and_broadcast():
         assert A == list(range(21)) and X == [float(i) for i in range(21)]
         assert LT == [0.0, 1.0, 2.0, 3.0, 4.0]
         assert c == [[3.0] * 4] and n == [[5.0] * 4]
+
+
+class _StubModel:
+    """Stands in for Chemeleon on the CPU: sample_states yields, for every t, states that encode the global
+    node / crystal indices and t, so the gathered batch shows whether every rank's slice landed in place.
+    It records the arguments the distributed sampler passed (global sizes, bases, the conditioning)."""
+
+    text_guide = True
+    hparams = {"text_dim": 4}
+    device = torch.device("cpu")
+    mask_lattice_matrix = torch.ones(3, 3, dtype=torch.bool)
+
+    def __init__(self):
+        self.calls = []
+
+    def _conditioning(self, texts, B, cond, null):
+        return cond.expand(B, -1).contiguous(), null.expand(B, -1).contiguous()
+
+    def sample_states(self, natoms, texts, cond_scale, step_lr, *, noise, seed, text_embeds, null_text_embeds, clone,
+                      node_base, graph_base, init, global_sizes, graph):
+        self.calls.append(dict(natoms=list(natoms), node_base=node_base, graph_base=graph_base,
+                               global_sizes=global_sizes, cond=text_embeds.clone(), noise=noise))
+        N, B = sum(natoms), len(natoms)
+        for t in range(3, -1, -1):
+            a = torch.arange(node_base, node_base + N) * 10 + t
+            x = torch.arange(node_base, node_base + N, dtype=torch.float32)[:, None].repeat(1, 3) + t
+            lat = torch.arange(graph_base, graph_base + B, dtype=torch.float32)[:, None, None].repeat(1, 3, 3) + t
+            yield t, a, x, lat
+
+
+def _sampler_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from chemeleon_amd.distributed import sample_states_distributed
+        nat = [3, 5, 2, 7, 4, 6]
+        m = _StubModel()
+        cond = torch.full((1, 4), 3.0) if rank == 0 else torch.zeros(1, 4)  # only rank 0 holds the encoder output
+        null = torch.full((1, 4), 5.0) if rank == 0 else torch.zeros(1, 4)
+        every = [(t, a.tolist(), x[:, 0].tolist(), lat[:, 0, 0].tolist())
+                 for t, a, x, lat in sample_states_distributed(m, nat, None, noise="torch", text_embeds=cond,
+                                                               null_text_embeds=null, every_step=True)]
+        final = [t for t, *_ in sample_states_distributed(m, nat, None, noise="torch", text_embeds=cond,
+                                                            null_text_embeds=null)]
+        q.put((rank, every, final, m.calls[0]["global_sizes"], m.calls[0]["node_base"], m.calls[0]["graph_base"],
+               m.calls[0]["cond"][:, 0].tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_sampler_gathers_the_whole_batch_on_every_rank():
+    """sample_states_distributed (the path Chemeleon.sample() takes under a process group): every rank gets
+    the whole batch in global order at every step (every_step=True) or only the final one; each rank samples
+    its Σn²-balanced slice with the GLOBAL sizes and its node / crystal bases (the parity-mode noise slicing),
+    and the conditioning held by rank 0 reaches every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sampler_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    nat = [3, 5, 2, 7, 4, 6]
+    parts = partition(nat, 2)
+    for rank, every, final, gsz, nb, gb, cond in res:
+        assert [t for t, *_ in every] == [3, 2, 1, 0] and final == [0]
+        for t, a, x, lat in every:
+            assert a == [i * 10 + t for i in range(sum(nat))]
+            assert x == [float(i + t) for i in range(sum(nat))]
+            assert lat == [float(g + t) for g in range(len(nat))]
+        g0 = parts[rank][0]
+        assert gsz == (sum(nat), len(nat)) and gb == g0 and nb == sum(nat[:g0])
+        assert cond == [3.0] * (parts[rank][1] - g0)
