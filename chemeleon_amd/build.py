@@ -67,5 +67,32 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+# The torch-op layer (csrc/torch_ops.cpp: TORCH_LIBRARY(chemeleon) over the C ABI), built against this
+# torch's headers and libraries next to libchemeleon_hip.so (which it links, rpath $ORIGIN).
+OPS_SRC = os.path.join(CSRC, "torch_ops.cpp")
+OPS_LIB = os.path.join(os.path.dirname(LIB), "libchemeleon_torch_ops.so")
+
+
+def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
+    if not force and os.path.exists(OPS_LIB) and os.path.getmtime(OPS_LIB) >= max(
+            os.path.getmtime(OPS_SRC), os.path.getmtime(LIB)):
+        return OPS_LIB
+    import torch
+    import torch.utils.cpp_extension as ce
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    tmp = OPS_LIB + ".tmp"
+    cmd = ([hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+            f"-D_GLIBCXX_USE_CXX11_ABI={abi}"] + [f"-I{p}" for p in ce.include_paths()] +
+           [OPS_SRC, "-o", tmp, f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip",
+            f"-L{os.path.dirname(LIB)}", "-lchemeleon_hip", "-Wl,-rpath,$ORIGIN"])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(tmp, OPS_LIB)
+    return OPS_LIB
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_torch_ops(force="--force" in sys.argv)
