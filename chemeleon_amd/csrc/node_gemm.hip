@@ -162,15 +162,18 @@ __device__ __forceinline__ void node_epilogue_split(const GemmArgs& g, f32x16 (&
 // PS (S16 only): A arrives pre-split (GemmArgs::aex): its fragments are read from LDS as they are, the
 // accumulators are rescaled by 2^(e_prev - e_next) where a 128-column chunk of K ends (exact), and the
 // epilogue can write C split the same way (GemmArgs::Cs).
-template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false>
+// NSTO: ring depth override (deep rings for short grids, where each block's K loop is one latency chain)
+template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false, int NSTO = 0>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
-  static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4), "tiling");
+  static_assert(NSTO ? S16 && NB * NSTO * STB<true, NMT> <= 160 * 1024
+                     : NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4),
+                "tiling");
   static_assert(!PS || S16, "pre-split A is a split16 form");
   constexpr int NM = NMT, NI = NMT / 64;  // tile rows; 32-row fragment groups per wave
   constexpr int A_STB_ = A_STB<NMT>;
   // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
   // step t's barrier it takes tile t + NST while tiles t+1 .. t+NST-1 are in flight or landed.
-  constexpr int STB_ = STB<S16, NMT>, NST_ = NST<S16, NB, NMT>, AHEAD = NST_;
+  constexpr int STB_ = STB<S16, NMT>, NST_ = NSTO ? NSTO : NST<S16, NB, NMT>, AHEAD = NST_;
   constexpr int GL = S16 ? 2 + NI : 5;                                   // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -476,7 +479,17 @@ int g_node_variant = 0;
 constexpr int LDS3 = STB<true> * NST<true, 3>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
 
+// deep-ring variants: {tile rows, blocks per CU, stages}
+#define CHM_NODE_DEEP(X) X(64, 2, 6) X(64, 1, 12) X(128, 1, 9) X(128, 2, 4)
+
 static hipError_t node_gemm_init_once() {
+#define CHM_DEEP_ATTR(R, B, S)                                                                                   \
+  if (hipError_t e = hipFuncSetAttribute((const void*)k_node_gemm<0, true, B, R, false, S>,                     \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, STB<true, R> * S);          \
+      e != hipSuccess)                                                                                          \
+    return e;
+  CHM_NODE_DEEP(CHM_DEEP_ATTR)
+#undef CHM_DEEP_ATTR
   const void* ks[14] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
                         (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
                         (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
@@ -499,6 +512,7 @@ hipError_t node_gemm_init() {
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
 int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
+int g_node_stages = 0;  // S16 deep-ring override (microbenchmarks): 0 = default, else a CHM_NODE_DEEP stage count
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
@@ -532,6 +546,18 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
       hipLaunchKernelGGL((k_node_gemm<0, true, 2, 128, true>), grid, block, NODE_LDS, s, g);
     }
     return hipGetLastError();
+  }
+  if (g.wscale && g_node_stages) {
+    const int nb = g_node_blocks ? g_node_blocks : 1;
+    const dim3 gridr((unsigned)(((g.M + rows - 1) / rows) * (g.N / NN)));
+#define CHM_DEEP_LAUNCH(R, B, S)                                                                         \
+  if (rows == R && nb == B && g_node_stages == S) {                                                      \
+    hipLaunchKernelGGL((k_node_gemm<0, true, B, R, false, S>), gridr, block, (STB<true, R> * S), s, g);   \
+    return hipGetLastError();                                                                            \
+  }
+    CHM_NODE_DEEP(CHM_DEEP_LAUNCH)
+#undef CHM_DEEP_LAUNCH
+    return hipErrorInvalidValue;
   }
   if (g.wscale && rows == 64) {
     const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));

@@ -169,6 +169,31 @@ int main(int argc, char** argv) {
     printf("empty kernel, 160 blocks: %.2f us per launch\n", te * 1e3);
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "nodedeep") {  // split16 node GEMM: default ring vs deep rings
+    CK(node_gemm_init());
+    void* W16; float* wsc16; float* amax;
+    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
+    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
+    std::vector<float> one(M, 1.0f);
+    CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
+    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax;
+    const size_t nc = (size_t)M * N;
+    std::vector<float> c0(nc), c1(nc);
+    CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(c0.data(), C, nc * 4, hipMemcpyDeviceToHost));
+    const int cfg[][3] = {{0, 0, 0}, {64, 2, 6}, {64, 1, 12}, {128, 1, 9}, {128, 2, 4}};
+    for (int rep = 0; rep < 2; ++rep)
+      for (auto& c : cfg) {
+        g_node_rows = c[0]; g_node_blocks = c[1]; g_node_stages = c[2];
+        float t = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c1.data(), C, nc * 4, hipMemcpyDeviceToHost));
+        printf("M=%ld N=%d K=%d rows %d blocks/CU %d stages %d: %.2f us %.1f TF fp32-eq  bit-identical %s\n", M, N, K,
+               c[0], c[1], c[2], t * 1e3, flops / t / 1e9, c0 == c1 ? "yes" : "NO");
+      }
+    g_node_rows = g_node_blocks = g_node_stages = 0;
+    return 0;
+  }
   if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
     CK(node_gemm_init());
     for (int rep = 0; rep < 2; ++rep) {
