@@ -84,6 +84,8 @@ SIGNATURES = {
     "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
     "chm_batch_num_nodes": (c_i64, [c_void_p]),
     "chm_batch_num_edges": (c_i64, [c_void_p]),
+    "chm_batch_info": (c_int, [c_void_p, ctypes.POINTER(chm_dims), ctypes.POINTER(c_i64), ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_int)]),
     "chm_decoder_forward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "chm_sample_step": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_int, c_float, c_void_p, c_void_p, c_void_p,

@@ -1044,8 +1044,8 @@ hipError_t xcd_mask(int blocks, unsigned* out) {
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpy(out, d, sizeof(unsigned), hipMemcpyDeviceToHost);
-  hipFree(d);
-  return e;
+  const hipError_t ef = hipFree(d);
+  return e != hipSuccess ? e : ef;
 }
 
 // Repair of a k_edge16_layer launch whose check failed (*g.xbad != 0: some layer-2 tile read S written

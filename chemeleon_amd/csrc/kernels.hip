@@ -591,37 +591,38 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
   const float eps = 1.0e-6f;
   if (d_t) t_const = *d_t;
   for (long i = (long)blockIdx.x * 4 + wv; i < N; i += (long)gridDim.x * 4) {
-    const int t = tnode ? (int)tnode[i] : t_const;
+    // (indices from callers are clamped into the tables: t to [1, T], x_t to [0, A); the sampler's are in range)
+    const int t = min(max(tnode ? (int)tnode[i] : t_const, 1), T);
     const int d0 = lane, d1 = lane + 64;
-    const bool ok1 = d1 < A;
-    float lg0 = L1[i * ld + d0];
+    const bool ok0 = d0 < A, ok1 = d1 < A;
+    float lg0 = ok0 ? L1[i * ld + d0] : -INFINITY;
     float lg1 = ok1 ? L1[i * ld + d1] : -INFINITY;
     if (L2) {
-      lg0 = __fadd_rn(__fmul_rn(w1, L2[i * ld + d0]), __fmul_rn(w2, lg0));
+      if (ok0) lg0 = __fadd_rn(__fmul_rn(w1, L2[i * ld + d0]), __fmul_rn(w2, lg0));
       if (ok1) lg1 = __fadd_rn(__fmul_rn(w1, L2[i * ld + d1]), __fmul_rn(w2, lg1));
     }
     // softmax over the A classes
     const float mx = wave_max(fmaxf(lg0, lg1));
-    const float e0 = expf(lg0 - mx), e1 = ok1 ? expf(lg1 - mx) : 0.f;
+    const float e0 = ok0 ? expf(lg0 - mx) : 0.f, e1 = ok1 ? expf(lg1 - mx) : 0.f;
     const float inv = 1.0f / wave_sum(e0 + e1);
-    sm[d0] = e0 * inv;
+    if (ok0) sm[d0] = e0 * inv;
     if (ok1) sm[d1] = e1 * inv;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    const int x = (int)xt[i];
+    const int x = (int)min(max(xt[i], (int64_t)0), (int64_t)(A - 1));
     const long t1 = t - 1;
     const long t2 = (t - 2 + (T + 1)) % (T + 1);
     const float* Q2 = qm + t2 * A * A;
     float f20 = 0.f, f21 = 0.f;
     for (int cc = 0; cc < A; ++cc) {
       const float p = sm[cc];
-      f20 = fmaf(p, Q2[cc * A + d0], f20);
+      if (ok0) f20 = fmaf(p, Q2[cc * A + d0], f20);
       if (ok1) f21 = fmaf(p, Q2[cc * A + d1], f21);
     }
     const float* Q1 = q1 + t1 * A * A;
-    float v0, v1 = -INFINITY;
+    float v0 = -INFINITY, v1 = -INFINITY;
     const float nz = (t != 1) ? 1.0f : 0.0f;
-    {
+    if (ok0) {
       float post = (t == 1) ? lg0 : __fadd_rn(logf(Q1[d0 * A + x] + eps), logf(f20 + eps));
       float u = noise ? noise[i * A + d0] : rng_uniform(seed, t, 0, (uint64_t)(i + node_base) * 128 + d0);
       u = fminf(fmaxf(u, eps), 1.0f);
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
       v1 = __fadd_rn(post, __fmul_rn(gmb, nz));
     }
     float bv = v0;
-    int bi = d0;
+    int bi = ok0 ? d0 : 1 << 30;
     if (ok1 && better(v1, d1, bv, bi)) { bv = v1; bi = d1; }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

@@ -954,6 +954,14 @@ extern "C" void chm_batch_destroy(chm_batch* b) {
 extern "C" size_t chm_batch_device_bytes(const chm_batch* b) { return b ? b->bytes : 0; }
 extern "C" int64_t chm_batch_num_nodes(const chm_batch* b) { return b ? b->N : -1; }
 extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -1; }
+extern "C" int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn) {
+  if (!b) return fail(CHM_E_ARG, "batch is NULL");
+  if (dims) *dims = b->m->d;
+  if (num_graphs) *num_graphs = b->B;
+  if (max_pairs) *max_pairs = b->P;
+  if (knn) *knn = b->knn;
+  return CHM_OK;
+}
 
 // ---------------------------------------------------------------- instrumentation
 namespace {
@@ -1427,6 +1435,7 @@ extern "C" int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sc, in
 extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, float* agg, void* stream) {
   if (!b || !msg || !agg) return fail(CHM_E_ARG, "NULL argument");
   if (pairs < 1) return fail(CHM_E_ARG, "pairs must be >= 1");
+  if (b->knn) return fail(CHM_E_UNSUPPORTED, "segment_mean: the fc edge layout only (knn edges change per call)");
   HIPCHK(segment_mean(msg, agg, b->n2g, b->node_off, b->edge_off, b->natoms, b->N, b->E, pairs, (hipStream_t)stream));
   return CHM_OK;
 }

@@ -36,34 +36,71 @@ const float* fptr(const c10::optional<at::Tensor>& t, const char* name) {
   return t->data_ptr<float>();
 }
 
-chm_batch* batch_of(int64_t handle) {
+// A batch handle with its model's dimensions: every tensor is checked against these on the host before a
+// launch (the kernels trust their sizes: a mis-sized tensor would be an out-of-bounds access on the device)
+struct Batch {
+  chm_batch* b;
+  chm_dims d;
+  int64_t N, E, B;
+  int P, knn;
+};
+
+Batch batch_of(int64_t handle) {
   TORCH_CHECK(handle != 0, "batch handle is 0");
-  return reinterpret_cast<chm_batch*>(handle);
+  Batch r{};
+  r.b = reinterpret_cast<chm_batch*>(handle);
+  check(chm_batch_info(r.b, &r.d, &r.B, &r.P, &r.knn), "chm_batch_info");
+  r.N = chm_batch_num_nodes(r.b);
+  r.E = chm_batch_num_edges(r.b);
+  return r;
+}
+
+void need_shape(const at::Tensor& t, at::IntArrayRef shape, const char* name) {
+  TORCH_CHECK(t.sizes() == shape, name, ": expected shape ", shape, ", got ", t.sizes());
+}
+
+void need_state(const Batch& b, const at::Tensor& a, const at::Tensor& x, const at::Tensor& l) {
+  need(a, at::kLong, "atom_types");
+  need(x, at::kFloat, "frac");
+  need(l, at::kFloat, "lattices");
+  need_shape(a, {b.N}, "atom_types");
+  need_shape(x, {b.N, 3}, "frac");
+  need_shape(l, {b.B, 3, 3}, "lattices");
+  TORCH_CHECK(a.device() == x.device() && a.device() == l.device(), "state tensors on different devices");
 }
 
 // CSPNet.forward for `pairs` conditionings sharing atoms / coordinates / lattices (pairs = 2: the CFG pair
-// of Chemeleon.model_predictions): -> (types [pairs,N,A], lattice [pairs,B,3,3], coords [pairs,N,3],
-// node features [pairs,N,H])
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decoder_forward(
-    int64_t batch, int64_t pairs, const at::Tensor& atom_types, const at::Tensor& frac, const at::Tensor& lattices,
-    const c10::optional<at::Tensor>& time_emb, int64_t time_stride, const c10::optional<at::Tensor>& text,
-    int64_t max_atoms, int64_t hidden) {
-  chm_batch* b = batch_of(batch);
-  const int64_t N = chm_batch_num_nodes(b);
-  need(atom_types, at::kLong, "atom_types");
-  need(frac, at::kFloat, "frac");
-  need(lattices, at::kFloat, "lattices");
-  TORCH_CHECK(atom_types.numel() == N && frac.numel() == 3 * N, "atom_types / frac do not match the batch's ", N,
-              " nodes");
-  TORCH_CHECK(lattices.dim() == 3 && lattices.size(1) == 3 && lattices.size(2) == 3, "lattices must be [B,3,3]");
-  const int64_t B = lattices.size(0);
+// of Chemeleon.model_predictions): time_emb [B, >= time_dim] (row stride = its last size), text
+// [pairs, B, text_dim] -> (types [pairs,N,max_atoms], lattice [pairs,B,3,3], coords [pairs,N,3],
+// node features [pairs,N,hidden_dim])
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decoder_forward(int64_t batch, int64_t pairs,
+                                                                           const at::Tensor& atom_types,
+                                                                           const at::Tensor& frac,
+                                                                           const at::Tensor& lattices,
+                                                                           const c10::optional<at::Tensor>& time_emb,
+                                                                           const c10::optional<at::Tensor>& text) {
+  const Batch b = batch_of(batch);
+  TORCH_CHECK(pairs >= 1 && pairs <= b.P, "pairs must be in [1, ", b.P, "] for this batch");
+  need_state(b, atom_types, frac, lattices);
+  const bool film = b.d.time_dim > 0 || b.d.text_dim > 0;
+  int64_t tstride = 0;
+  if (film) {
+    TORCH_CHECK(time_emb.has_value(), "time_emb is required (the model has a FiLM layer)");
+    TORCH_CHECK(time_emb->dim() == 2 && time_emb->size(0) == b.B && time_emb->size(1) >= b.d.time_dim,
+                "time_emb must be [B, >= time_dim]");
+    tstride = time_emb->size(1);
+  }
+  if (b.d.text_dim > 0) {
+    TORCH_CHECK(text.has_value(), "text embeddings are required (text_dim > 0)");
+    need_shape(*text, {pairs, b.B, b.d.text_dim}, "text");
+  }
   auto o = frac.options();
-  at::Tensor types = at::empty({pairs, N, max_atoms}, o), latt = at::empty({pairs, B, 3, 3}, o),
-             coords = at::empty({pairs, N, 3}, o), nodes = at::empty({pairs, N, hidden}, o);
-  check(chm_decoder_forward(b, (int)pairs, atom_types.data_ptr<int64_t>(), frac.data_ptr<float>(),
-                            lattices.data_ptr<float>(), fptr(time_emb, "time_emb"), (int)time_stride,
-                            fptr(text, "text"), types.data_ptr<float>(), latt.data_ptr<float>(),
-                            coords.data_ptr<float>(), nodes.data_ptr<float>(), stream()),
+  at::Tensor types = at::empty({pairs, b.N, b.d.max_atoms}, o), latt = at::empty({pairs, b.B, 3, 3}, o),
+             coords = at::empty({pairs, b.N, 3}, o), nodes = at::empty({pairs, b.N, b.d.hidden_dim}, o);
+  check(chm_decoder_forward(b.b, (int)pairs, atom_types.data_ptr<int64_t>(), frac.data_ptr<float>(),
+                            lattices.data_ptr<float>(), film ? fptr(time_emb, "time_emb") : nullptr, (int)tstride,
+                            b.d.text_dim > 0 ? fptr(text, "text") : nullptr, types.data_ptr<float>(),
+                            latt.data_ptr<float>(), coords.data_ptr<float>(), nodes.data_ptr<float>(), stream()),
         "chm_decoder_forward");
   return {types, latt, coords, nodes};
 }
@@ -76,19 +113,27 @@ void sample_step(int64_t batch, int64_t schedule, int64_t t, double cond_scale, 
                  const c10::optional<at::Tensor>& null, const c10::optional<at::Tensor>& rand_a,
                  const c10::optional<at::Tensor>& rand_l, const c10::optional<at::Tensor>& rand_x1,
                  const c10::optional<at::Tensor>& rand_x2, int64_t seed, int64_t node_base, int64_t graph_base) {
-  chm_batch* b = batch_of(batch);
+  const Batch b = batch_of(batch);
+  TORCH_CHECK(b.P >= 2, "sample_step needs a batch created for 2 pairs (the CFG pair)");
   TORCH_CHECK(schedule != 0, "schedule is 0");
-  const int64_t N = chm_batch_num_nodes(b);
-  need(atom_types, at::kLong, "atom_types");
-  need(frac, at::kFloat, "frac");
-  need(lattices, at::kFloat, "lattices");
-  TORCH_CHECK(atom_types.numel() == N && frac.numel() == 3 * N, "state does not match the batch's ", N, " nodes");
+  need_state(b, atom_types, frac, lattices);
+  const bool guide = b.d.text_dim > 0;
+  TORCH_CHECK(cond.has_value() == guide && null.has_value() == guide,
+              guide ? "cond and null text embeddings are required" : "this model takes no text embeddings");
+  if (guide) {
+    need_shape(*cond, {b.B, b.d.text_dim}, "cond");
+    need_shape(*null, {b.B, b.d.text_dim}, "null");
+  }
   const bool noise = rand_a.has_value();
   TORCH_CHECK(noise == rand_l.has_value() && noise == rand_x1.has_value() && noise == rand_x2.has_value(),
               "pass all four noise tensors (parity mode) or none (device noise)");
-  if (noise) TORCH_CHECK(rand_a->numel() % N == 0 && rand_x1->numel() == 3 * N && rand_x2->numel() == 3 * N,
-                         "noise tensors do not match the batch");
-  check(chm_sample_step(b, reinterpret_cast<const chm_schedule*>(schedule), (int)t, (float)cond_scale,
+  if (noise) {
+    need_shape(*rand_a, {b.N, b.d.max_atoms}, "rand_a");
+    need_shape(*rand_l, {b.B, 3, 3}, "rand_l");
+    need_shape(*rand_x1, {b.N, 3}, "rand_x1");
+    need_shape(*rand_x2, {b.N, 3}, "rand_x2");
+  }
+  check(chm_sample_step(b.b, reinterpret_cast<const chm_schedule*>(schedule), (int)t, (float)cond_scale,
                         atom_types.data_ptr<int64_t>(), frac.data_ptr<float>(), lattices.data_ptr<float>(),
                         fptr(cond, "cond"), fptr(null, "null"), fptr(rand_a, "rand_a"), fptr(rand_l, "rand_l"),
                         fptr(rand_x1, "rand_x1"), fptr(rand_x2, "rand_x2"), (uint64_t)seed, node_base, graph_base,
@@ -96,14 +141,15 @@ void sample_step(int64_t batch, int64_t schedule, int64_t t, double cond_scale, 
         "chm_sample_step");
 }
 
-// scatter_mean of per-edge messages [pairs,E,H] onto their source nodes -> [pairs,N,H]
+// scatter_mean of per-edge messages [pairs,E,hidden_dim] onto their source nodes -> [pairs,N,hidden_dim]
 at::Tensor segment_mean(int64_t batch, int64_t pairs, const at::Tensor& msg) {
-  chm_batch* b = batch_of(batch);
+  const Batch b = batch_of(batch);
+  TORCH_CHECK(!b.knn, "segment_mean: fc batches only");
+  TORCH_CHECK(pairs >= 1, "pairs must be >= 1");
   need(msg, at::kFloat, "msg");
-  const int64_t E = chm_batch_num_edges(b), N = chm_batch_num_nodes(b);
-  TORCH_CHECK(msg.dim() == 3 && msg.size(0) == pairs && msg.size(1) == E, "msg must be [pairs, E, H]");
-  at::Tensor agg = at::empty({pairs, N, msg.size(2)}, msg.options());
-  check(chm_segment_mean(b, (int)pairs, msg.data_ptr<float>(), agg.data_ptr<float>(), stream()), "chm_segment_mean");
+  need_shape(msg, {pairs, b.E, b.d.hidden_dim}, "msg");
+  at::Tensor agg = at::empty({pairs, b.N, b.d.hidden_dim}, msg.options());
+  check(chm_segment_mean(b.b, (int)pairs, msg.data_ptr<float>(), agg.data_ptr<float>(), stream()), "chm_segment_mean");
   return agg;
 }
 
@@ -118,6 +164,7 @@ at::Tensor d3pm_sample(const at::Tensor& logits, const at::Tensor& xt, const at:
   need(q_mats, at::kFloat, "q_mats");
   TORCH_CHECK(logits.dim() == 2 && noise.sizes() == logits.sizes(), "logits / noise must be [N, A]");
   const int64_t N = logits.size(0), A = logits.size(1);
+  TORCH_CHECK(A >= 1 && A <= 128, "at most 128 classes");
   TORCH_CHECK(xt.numel() == N && t.numel() == N, "x_t / t must have N entries");
   TORCH_CHECK(q_mats.dim() == 3 && q_mats.size(1) == A && q_mats.size(2) == A && q_one_step.sizes() == q_mats.sizes(),
               "q tables must be [T+1, A, A]");
@@ -133,7 +180,7 @@ at::Tensor d3pm_sample(const at::Tensor& logits, const at::Tensor& xt, const at:
 
 TORCH_LIBRARY(chemeleon, m) {
   m.def("decoder_forward(int batch, int pairs, Tensor atom_types, Tensor frac, Tensor lattices, Tensor? time_emb, "
-        "int time_stride, Tensor? text, int max_atoms, int hidden) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor? text) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("sample_step(int batch, int schedule, int t, float cond_scale, Tensor(a!) atom_types, Tensor(b!) frac, "
         "Tensor(c!) lattices, Tensor? cond, Tensor? null, Tensor? rand_a, Tensor? rand_l, Tensor? rand_x1, "
         "Tensor? rand_x2, int seed, int node_base, int graph_base) -> ()");

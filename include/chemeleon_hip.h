@@ -259,7 +259,8 @@ int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sched, int32_t* d
 /* Standalone message-passing aggregation (scatter_mean of edge messages onto
  * their source node; chemeleon/utils/scatter.py:88-112 as called from
  * cspnet.py:155-160) over this batch's fc edge layout:
- *   d_msg [pairs,E,H] -> d_agg [pairs,N,H], agg[i] = sum_j msg[(i,j)] / max(n_g,1). */
+ *   d_msg [pairs,E,H] -> d_agg [pairs,N,H], agg[i] = sum_j msg[(i,j)] / max(n_g,1),
+ * H = hidden_dim (512); fc batches only (CHM_E_UNSUPPORTED for knn). */
 int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, float* d_agg, void* stream);
 
 /* D3PM reverse sampling for explicit inputs (diff_utils.py:307-329):
@@ -361,6 +362,12 @@ int chm_mt19937_uniform(uint32_t* state, int32_t* left, int32_t* next, int64_t c
 /* Sizes of the batch (for callers that allocate outputs). */
 int64_t chm_batch_num_nodes(const chm_batch* b);
 int64_t chm_batch_num_edges(const chm_batch* b);
+
+/* The model dimensions behind a batch and its sizes (any pointer may be NULL): *dims = the
+ * model's chm_dims, *num_graphs = B, *max_pairs = the pairs it was created for, *knn = 1 for a
+ * knn-edge batch. Callers that allocate outputs or validate shapes use it (the torch-op layer,
+ * chemeleon_amd/csrc/torch_ops.cpp, checks every tensor against it before a launch). */
+int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn);
 
 #ifdef __cplusplus
 }

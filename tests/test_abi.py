@@ -54,6 +54,7 @@ def test_null_handles_are_rejected():
     lib = _lib.load()
     assert lib.chm_decoder_forward(None, 1, None, None, None, None, 0, None, None, None, None, None, None) == -1
     assert lib.chm_segment_mean(None, 1, None, None, None) == -1
+    assert lib.chm_batch_info(None, None, None, None, None) == -1
     assert lib.chm_d3pm_sample(-1, 104, 100, *([None] * 8)) == -1
     assert lib.chm_batch_num_nodes(None) == -1
 

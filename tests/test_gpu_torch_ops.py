@@ -51,7 +51,7 @@ def test_decoder_forward_op_matches_ctypes(model, chem):
     tx = c.expand(B, -1).to(DEV).contiguous()
     ref = dec._run(1, a, x, lat, NAT, te, tx)
     b = dec.hip_batch(NAT, max_pairs=1)
-    got = chem.decoder_forward(ops.handle(b), 1, a, x, lat, te, dec.time_dim, tx, dec.max_atoms, dec.hidden_dim)
+    got = chem.decoder_forward(ops.handle(b), 1, a, x, lat, te, tx.unsqueeze(0))
     torch.cuda.synchronize()
     for r, o in zip(ref, got):
         assert torch.equal(r, o)
@@ -86,7 +86,7 @@ def test_segment_mean_op_matches_oracle(model, chem):
     from oracle import chemeleon_oracle as O
     b = model.decoder.hip_batch(NAT, max_pairs=2)
     g = torch.Generator().manual_seed(3)
-    msg = torch.randn(2, b.num_edges, 64, generator=g)
+    msg = torch.randn(2, b.num_edges, 512, generator=g)
     agg = chem.segment_mean(ops.handle(b), 2, msg.to(DEV))
     e = O.fc_edges(NAT)
     for k in range(2):
@@ -103,11 +103,33 @@ def test_d3pm_sample_op_bit_exact(model, chem, golden):
 
 
 def test_ops_check_shapes_before_launch(model, chem):
+    """Every tensor is checked against the batch's sizes and the model's dimensions (chm_batch_info) on the
+    host: a mis-sized tensor raises RuntimeError and nothing is launched."""
     a, x, lat = _state()
-    b = model.decoder.hip_batch(NAT, max_pairs=1)
-    with pytest.raises(RuntimeError, match="do not match"):
-        chem.decoder_forward(ops.handle(b), 1, a[:-1], x, lat, None, 0, None, 100, 512)
+    B = len(NAT)
+    b = model.decoder.hip_batch(NAT, max_pairs=2)
+    h = ops.handle(b)
+    te = torch.zeros(B, 128, device=DEV)
+    tx = torch.zeros(1, B, 512, device=DEV)
+    with pytest.raises(RuntimeError, match="atom_types: expected shape"):
+        chem.decoder_forward(h, 1, a[:-1], x, lat, te, tx)
+    with pytest.raises(RuntimeError, match="time_emb"):
+        chem.decoder_forward(h, 1, a, x, lat, te[:, :64], tx)
+    with pytest.raises(RuntimeError, match="text: expected shape"):
+        chem.decoder_forward(h, 2, a, x, lat, te, tx)
+    with pytest.raises(RuntimeError, match="pairs must be in"):
+        chem.decoder_forward(h, 3, a, x, lat, te, tx.expand(3, -1, -1).contiguous())
+    with pytest.raises(RuntimeError, match="msg: expected shape"):
+        chem.segment_mean(h, 2, torch.zeros(2, b.num_edges, 64, device=DEV))
+    sched, _keep = model.schedule_tables(1e-5)
+    c = torch.zeros(B, 512, device=DEV)
     with pytest.raises(RuntimeError, match="all four noise tensors"):
-        sched, _keep = model.schedule_tables(1e-5)
-        chem.sample_step(ops.handle(b), ops.schedule_address(sched), 10, 2.0, a, x, lat, None, None,
-                         torch.zeros(1, device=DEV), None, None, None, 0, 0, 0)
+        chem.sample_step(h, ops.schedule_address(sched), 10, 2.0, a, x, lat, c, c, torch.zeros(1, device=DEV), None,
+                         None, None, 0, 0, 0)
+    with pytest.raises(RuntimeError, match="rand_a: expected shape"):
+        chem.sample_step(h, ops.schedule_address(sched), 10, 2.0, a, x, lat, c, c,
+                         torch.zeros(sum(NAT), 64, device=DEV), torch.zeros(B, 3, 3, device=DEV),
+                         torch.zeros(sum(NAT), 3, device=DEV), torch.zeros(sum(NAT), 3, device=DEV), 0, 0, 0)
+    with pytest.raises(RuntimeError, match="cond: expected shape"):
+        chem.sample_step(h, ops.schedule_address(sched), 10, 2.0, a, x, lat, c[:1], c, None, None, None, None, 0, 0, 0)
+    torch.cuda.synchronize()  # (nothing was launched: the stream is clean)

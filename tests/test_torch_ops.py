@@ -13,7 +13,7 @@ def test_ops_register_with_their_schemas():
     schemas = {name: str(getattr(chem, name).default._schema) for name in
                ("decoder_forward", "sample_step", "segment_mean", "d3pm_sample")}
     assert "Tensor(a!) atom_types" in schemas["sample_step"] and "-> ()" in schemas["sample_step"]
-    assert schemas["decoder_forward"].endswith("-> (Tensor, Tensor, Tensor, Tensor)")
+    assert schemas["decoder_forward"].endswith("Tensor? text) -> (Tensor, Tensor, Tensor, Tensor)")
     assert "Tensor msg" in schemas["segment_mean"]
     assert "Tensor q_mats" in schemas["d3pm_sample"]
 
