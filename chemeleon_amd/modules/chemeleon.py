@@ -506,6 +506,11 @@ class Chemeleon(nn.Module):
         sched, _keep = self.schedule_tables(step_lr)
         batch = self.decoder.hip_batch(natoms, max_pairs=2)
         nz = [None] * 4 if noise is None else [z.to(dev).float().contiguous() for z in noise]
+        N, B, A = sum(natoms), len(natoms), self.decoder.max_atoms
+        if a.shape != (N,) or x.shape != (N, 3) or lat.shape != (B, 3, 3):
+            raise ValueError("state shapes do not match natoms")
+        if noise is not None and [tuple(z.shape) for z in nz] != [(N, A), (B, 3, 3), (N, 3), (N, 3)]:
+            raise ValueError(f"noise must be (rand_a [N,{A}], rand_l [B,3,3], rand_x1 [N,3], rand_x2 [N,3])")
         _lib.require_device(a, x, lat, cond, null, *nz)
         _lib.check(_lib.load().chm_sample_step(batch.handle, sched, int(t), float(cond_scale), _lib.ptr(a),
                                                _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null),

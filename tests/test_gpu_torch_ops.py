@@ -65,7 +65,7 @@ def test_sample_step_op_matches_ctypes(model, chem, noise):
     c, n = c.expand(B, -1).to(DEV).contiguous(), n.expand(B, -1).to(DEV).contiguous()
     if noise == "explicit":
         g = torch.Generator().manual_seed(5)
-        nz = [torch.rand(N, 100, generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+        nz = [torch.rand(N, model.decoder.max_atoms, generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
               torch.randn(N, 3, generator=g)]
         nz = [z.to(DEV) for z in nz]
     else:
