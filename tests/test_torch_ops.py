@@ -25,3 +25,26 @@ def test_cpu_tensors_are_refused():
     with pytest.raises(NotImplementedError):
         chem.d3pm_sample(*[torch.zeros(2, 3)] * 2, torch.zeros(2, dtype=torch.long), torch.zeros(2, 3),
                          torch.zeros(4, 3, 3), torch.zeros(4, 3, 3))
+
+
+def test_load_fails_loudly_without_the_library(tmp_path):
+    import importlib
+    fresh = importlib.reload(ops)  # (a module whose registry has not loaded anything yet)
+    try:
+        with pytest.raises(ImportError, match="torch-op library not found"):
+            fresh.load(str(tmp_path / "missing.so"))
+    finally:
+        importlib.reload(ops)
+
+
+def test_handle_accepts_batches_handles_and_ints():
+    import ctypes
+
+    class FakeBatch:
+        handle = ctypes.c_void_p(1234)
+
+    assert ops.handle(FakeBatch()) == 1234
+    assert ops.handle(ctypes.c_void_p(99)) == 99
+    assert ops.handle(7) == 7
+    with pytest.raises(ValueError):
+        ops.handle(ctypes.c_void_p())
