@@ -80,6 +80,11 @@ def parse():
                    help="philox: device noise keyed by global index (the headline); torch: parity mode, the "
                         "reference's CPU RNG stream drawn on every rank at the global size, each rank uploading its "
                         "rows before every replay of the captured step (chemeleon_amd.noise)")
+    p.add_argument("--share", type=int, default=1, metavar="N",
+                   help="profiling: run, on this one GPU, the share of rank --share-rank of an N-rank job (the "
+                        "sharding of sample(): contiguous ranges balanced by sum of n^2); value then counts that "
+                        "share's structures")
+    p.add_argument("--share-rank", type=int, default=0)
     p.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)  # (the PMC passes' workload)
     return p.parse_args()
 
@@ -395,6 +400,15 @@ def main():
     else:
         all_nat = [args.n_atoms] * total
     ranges = partition(all_nat, world)
+    share_of = None
+    if args.share > 1:  # (profiling one rank's share of a larger job on this GPU)
+        if world > 1 or not 0 <= args.share_rank < args.share:
+            raise SystemExit("bench.py: --share runs one rank's share on ONE process (0 <= --share-rank < --share)")
+        r0, r1 = partition(all_nat, args.share)[args.share_rank]
+        share_of = (args.share_rank, args.share, total)
+        all_nat = all_nat[r0:r1]
+        total = len(all_nat)
+        ranges = [(0, total)]
     per = [b - a for a, b in ranges]
     g0 = ranges[rank][0]
     natoms = all_nat[ranges[rank][0]:ranges[rank][1]]
@@ -552,11 +566,11 @@ def main():
         L_ = _lib.load()
         st = _lib.stream_handle(dev)
         for _ in range(2):
-            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), _lib.ptr(agg), st), "segment_mean")
+            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), msg.numel(), _lib.ptr(agg), agg.numel(), st), "segment_mean")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), _lib.ptr(agg), st), "segment_mean")
+            _lib.check(L_.chm_segment_mean(b.handle, 2, _lib.ptr(msg), msg.numel(), _lib.ptr(agg), agg.numel(), st), "segment_mean")
         e1.record()
         torch.cuda.synchronize()
         seg_ms = e0.elapsed_time(e1) / 10
@@ -590,7 +604,11 @@ def main():
                    "noise": ("philox (device)" if args.noise == "philox" else
                              "torch (parity mode: the reference's CPU RNG stream at the global size on every rank, "
                              "this rank's rows uploaded before each replay)"),
-                   "launch": "eager" if args.no_graph else f"hip graph replay per step, {args.lanes} stream lane(s)"},
+                   "launch": "eager" if args.no_graph else f"hip graph replay per step, {args.lanes} stream lane(s)",
+                   "share": (None if share_of is None else
+                             f"rank {share_of[0]}'s share of a {share_of[1]}-rank job of {share_of[2]} crystals "
+                             f"({total} crystals, {sum(all_nat)} atoms, {sum(n * n for n in all_nat)} edges), run alone "
+                             "on one GPU; value counts this share's structures")},
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),

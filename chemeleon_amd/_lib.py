@@ -44,8 +44,47 @@ class chm_train_tables(ctypes.Structure):
 
 
 class chm_schedule(ctypes.Structure):
-    _fields_ = [("T", c_int), ("d_coef", c_void_p), ("d_time_emb", c_void_p), ("d_q_one_step", c_void_p),
-                ("d_q_mats", c_void_p)]
+    _fields_ = [("T", c_int), ("num_classes", c_int), ("time_dim", c_int), ("reserved", c_int),
+                ("d_coef", c_void_p), ("d_time_emb", c_void_p), ("d_q_one_step", c_void_p), ("d_q_mats", c_void_p)]
+
+
+class chm_step_io(ctypes.Structure):
+    """The buffers of one reverse step with their element counts (include/chemeleon_hip.h)."""
+    _fields_ = [("d_atom_types", c_void_p), ("n_atom_types", c_i64), ("d_frac", c_void_p), ("n_frac", c_i64),
+                ("d_lattices", c_void_p), ("n_lattices", c_i64), ("d_cond", c_void_p), ("n_cond", c_i64),
+                ("d_null", c_void_p), ("n_null", c_i64), ("d_rand_a", c_void_p), ("n_rand_a", c_i64),
+                ("d_rand_l", c_void_p), ("n_rand_l", c_i64), ("d_rand_x1", c_void_p), ("n_rand_x1", c_i64),
+                ("d_rand_x2", c_void_p), ("n_rand_x2", c_i64)]
+
+
+def step_io(a, x, lat, cond=None, null=None, noise=None, node0: int = 0, graph0: int = 0, nodes: int = None,
+            graphs: int = None):
+    """chm_step_io over tensors: the state (a [N] int64, x [N,3], lat [B,3,3]), conditioning rows
+    [B, text_dim] and the optional parity-mode noise (rand_a [N,A], rand_l [B,3,3], rand_x1, rand_x2 [N,3]).
+    With nodes / graphs given, the buffers are the rows [node0, node0 + nodes) / [graph0, graph0 + graphs)
+    of those tensors (one lane of a captured step); counts are element counts of those rows."""
+    nodes = a.shape[0] - node0 if nodes is None else nodes
+    graphs = lat.shape[0] - graph0 if graphs is None else graphs
+
+    def rows(t, first, n):
+        if t is None:
+            return None, 0
+        per = t[0].numel() if t.dim() > 1 else 1
+        return t.data_ptr() + first * per * t.element_size(), n * per
+
+    io = chm_step_io()
+    io.d_atom_types, io.n_atom_types = rows(a, node0, nodes)
+    io.d_frac, io.n_frac = rows(x, node0, nodes)
+    io.d_lattices, io.n_lattices = rows(lat, graph0, graphs)
+    io.d_cond, io.n_cond = rows(cond, graph0, graphs)
+    io.d_null, io.n_null = rows(null, graph0, graphs)
+    if noise is not None and noise[0] is not None:
+        ra, rl, rx1, rx2 = noise
+        io.d_rand_a, io.n_rand_a = rows(ra, node0, nodes)
+        io.d_rand_l, io.n_rand_l = rows(rl, graph0, graphs)
+        io.d_rand_x1, io.n_rand_x1 = rows(rx1, node0, nodes)
+        io.d_rand_x2, io.n_rand_x2 = rows(rx2, node0, nodes)
+    return io
 
 
 # name -> (restype, argtypes); every symbol declared in include/chemeleon_hip.h
@@ -84,19 +123,18 @@ SIGNATURES = {
     "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
     "chm_batch_num_nodes": (c_i64, [c_void_p]),
     "chm_batch_num_edges": (c_i64, [c_void_p]),
+    "chm_batch_device": (c_int, [c_void_p]),
     "chm_batch_info": (c_int, [c_void_p, ctypes.POINTER(chm_dims), ctypes.POINTER(c_i64), ctypes.POINTER(c_int),
                                ctypes.POINTER(c_int)]),
     "chm_decoder_forward": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "chm_sample_step": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_int, c_float, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_u64, c_i64, c_i64,
-                                c_void_p]),
-    "chm_sample_step_dt": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_u64, c_i64, c_i64, c_void_p]),
-    "chm_sample_step_dt_noise": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                         c_void_p, c_void_p]),
-    "chm_segment_mean": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "chm_sample_step": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_int, c_float, ctypes.POINTER(chm_step_io),
+                                c_u64, c_i64, c_i64, c_void_p]),
+    "chm_sample_step_dt": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float,
+                                   ctypes.POINTER(chm_step_io), c_u64, c_i64, c_i64, c_void_p]),
+    "chm_sample_step_dt_noise": (c_int, [c_void_p, ctypes.POINTER(chm_schedule), c_void_p, c_float,
+                                         ctypes.POINTER(chm_step_io), c_void_p]),
+    "chm_segment_mean": (c_int, [c_void_p, c_int, c_void_p, c_i64, c_void_p, c_i64, c_void_p]),
     "chm_d3pm_sample": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     "chm_edge_features": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -115,7 +115,8 @@ struct EdgeArgs {
             // bit 13 (tests, exact results) = k_edge16_tail's layer-1 tiles start ~10 ms late and its
             // segment tiles wait ~2^10 spins only (a real timeout: they read S before it is written);
             // bit 14 (profiling / tests, WRONG results after a failed check) = no repair launches behind
-            // k_edge16_tail or k_edge16_layer
+            // k_edge16_tail or k_edge16_layer; bits 15 / 16 (profiling) = layer-1 / layer-2 tiles read their A
+            // rows from the first 16 row tiles (L2-resident)
 };
 // Device event counters of the edge kernels (edge16.hip), cumulative over launches and graph replays
 // until chm_prof_events_reset: wait timeouts and repair launches that ran (each must read 0 in a
@@ -242,6 +243,6 @@ hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits,
                        float w1, float w2, const int64_t* xt, const int64_t* tnode, int t_const, const int* d_t,
                        const float* noise,
                        const float* q1, const float* qm, int64_t* out, uint64_t seed, int64_t node_base,
-                       hipStream_t s);
+                       hipStream_t s, int* bad = nullptr);  // bad: see k_d3pm (caller indices checked)
 
 }  // namespace chm

@@ -584,15 +584,26 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
                                               int t_const, const int* __restrict__ d_t,
                                               const float* __restrict__ noise,
                                               const float* __restrict__ q1, const float* __restrict__ qm,
-                                              int64_t* __restrict__ out, uint64_t seed, int64_t node_base) {
+                                              int64_t* __restrict__ out, uint64_t seed, int64_t node_base,
+                                              int* __restrict__ bad) {
   __shared__ float sm_all[4][128];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   float* sm = sm_all[wv];
   const float eps = 1.0e-6f;
   if (d_t) t_const = *d_t;
   for (long i = (long)blockIdx.x * 4 + wv; i < N; i += (long)gridDim.x * 4) {
-    // (indices from callers are clamped into the tables: t to [1, T], x_t to [0, A); the sampler's are in range)
-    const int t = min(max(tnode ? (int)tnode[i] : t_const, 1), T);
+    // caller indices (bad != null, chm_d3pm_sample): t outside [1, T] or x_t outside [0, A) records the
+    // lowest such node in *bad and writes -1; the sampler's own indices (bad == null) are in range by
+    // construction and only clamped, so that nothing can read outside the tables
+    const int64_t t_in = tnode ? tnode[i] : (int64_t)t_const, x_in = xt[i];
+    if (bad && (t_in < 1 || t_in > T || x_in < 0 || x_in >= A)) {
+      if (lane == 0) {
+        atomicMin(bad, (int)i);
+        out[i] = -1;
+      }
+      continue;
+    }
+    const int t = (int)min(max(t_in, (int64_t)1), (int64_t)T);
     const int d0 = lane, d1 = lane + 64;
     const bool ok0 = d0 < A, ok1 = d1 < A;
     float lg0 = ok0 ? L1[i * ld + d0] : -INFINITY;
@@ -609,7 +620,7 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
     if (ok1) sm[d1] = e1 * inv;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    const int x = (int)min(max(xt[i], (int64_t)0), (int64_t)(A - 1));
+    const int x = (int)min(max(x_in, (int64_t)0), (int64_t)(A - 1));
     const long t1 = t - 1;
     const long t2 = (t - 2 + (T + 1)) % (T + 1);
     const float* Q2 = qm + t2 * A * A;
@@ -653,13 +664,13 @@ __global__ __launch_bounds__(256) void k_d3pm(int N, int A, int T, const float* 
 hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits, const float* logits2, float w1,
                        float w2, const int64_t* xt, const int64_t* tnode, int t_const, const int* d_t,
                        const float* noise, const float* q1, const float* qm, int64_t* out, uint64_t seed,
-                       int64_t node_base, hipStream_t s) {
+                       int64_t node_base, hipStream_t s, int* bad) {
   if (A > 128 || A < 1) return hipErrorInvalidValue;
   long blocks = (N + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_d3pm, dim3((unsigned)blocks), dim3(256), 0, s, N, A, T, logits, ld_logits, logits2, w1, w2, xt,
-                     tnode, t_const, d_t, noise, q1, qm, out, seed, node_base);
+                     tnode, t_const, d_t, noise, q1, qm, out, seed, node_base, bad);
   return hipGetLastError();
 }
 

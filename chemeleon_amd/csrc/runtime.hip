@@ -86,6 +86,7 @@ struct chm_model {
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int ncu = 0;           // compute units of the device the model lives on
+  int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
   int edge_skip_xcd = -1;  // (tests) option edge_dyn_skip_xcd: the persistent kernel's blocks on that XCD exit
   int repair_grid = 0;   // CHM_REPAIR_GRID: blocks of the edge kernels' repair launches (default: ncu)
@@ -323,6 +324,7 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
+    m->device = dev;
     // k_edge16_layer_dyn gives each of 8 XCDs static rows: on a device or partition mode with fewer XCDs
     // it would leave rows to its self-check and repair launches, so it runs only where 8 were seen
     if (m->ncu > 0 && xcd_mask(8 * m->ncu, &m->xcd_mask) != hipSuccess) m->xcd_mask = 0;
@@ -740,7 +742,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->M = b->math == MATH_F32 ? fl((size_t)P * E * H) : nullptr;
   b->rowmax = b->math == MATH_SPLIT16 ? (unsigned*)fl((size_t)P * E) : nullptr;
   b->rmx = fl((size_t)4 * P * N);
-  if (b->math == MATH_SPLIT16) {
+  if (b->math == MATH_SPLIT16 && m->node_ps) {  // (option node_ps at batch creation: ~335 MB at 512x40, P = 2)
     void** sp[4] = {&b->Hs, &b->Hls, &b->aggs, &b->Us};
     int** se[4] = {&b->He, &b->Hle, &b->agge, &b->Ue};
     for (int k = 0; k < 4; ++k) {
@@ -954,6 +956,7 @@ extern "C" void chm_batch_destroy(chm_batch* b) {
 extern "C" size_t chm_batch_device_bytes(const chm_batch* b) { return b ? b->bytes : 0; }
 extern "C" int64_t chm_batch_num_nodes(const chm_batch* b) { return b ? b->N : -1; }
 extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -1; }
+extern "C" int chm_batch_device(const chm_batch* b) { return b ? b->m->device : fail(CHM_E_ARG, "batch is NULL"); }
 extern "C" int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn) {
   if (!b) return fail(CHM_E_ARG, "batch is NULL");
   if (dims) *dims = b->m->d;
@@ -1373,21 +1376,62 @@ extern "C" int chm_decoder_forward(chm_batch* b, int pairs, const int64_t* a, co
   return CHM_OK;
 }
 
-static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, float cond_scale, int64_t* d_a,
-                       float* d_x, float* d_l, const float* d_cond, const float* d_null, const float* ra,
-                       const float* rl, const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
-                       int64_t graph_base, hipStream_t s) {
+// the element counts of a step's buffers against the batch (N nodes, B crystals) and its model
+static int check_step_io(const chm_batch* b, const chm_step_io* io, bool noise_required, bool noise_allowed) {
+  if (!io) return fail(CHM_E_ARG, "io is NULL");
+  const long N = b->N, B = b->B, A = b->m->d.max_atoms, X = b->m->d.text_dim;
+  auto want = [&](const void* p, int64_t n, long expect, const char* name) -> int {
+    if (!p) return fail(CHM_E_ARG, std::string(name) + " is NULL");
+    if (n != expect)
+      return fail(CHM_E_ARG, std::string(name) + ": " + std::to_string(n) + " elements, the batch needs " +
+                                 std::to_string(expect));
+    return CHM_OK;
+  };
+  int rc;
+  if ((rc = want(io->d_atom_types, io->n_atom_types, N, "atom_types [N]"))) return rc;
+  if ((rc = want(io->d_frac, io->n_frac, 3 * N, "frac [N,3]"))) return rc;
+  if ((rc = want(io->d_lattices, io->n_lattices, 9 * B, "lattices [B,3,3]"))) return rc;
+  if (X > 0) {
+    if ((rc = want(io->d_cond, io->n_cond, B * X, "cond [B,text_dim]"))) return rc;
+    if ((rc = want(io->d_null, io->n_null, B * X, "null [B,text_dim]"))) return rc;
+  }
+  const int given = (io->d_rand_a != nullptr) + (io->d_rand_l != nullptr) + (io->d_rand_x1 != nullptr) +
+                    (io->d_rand_x2 != nullptr);
+  if (given != 0 && given != 4) return fail(CHM_E_ARG, "noise: all four buffers or none");
+  if (given && !noise_allowed) return fail(CHM_E_ARG, "this entry point draws device noise: the noise buffers must be NULL");
+  if (!given && noise_required) return fail(CHM_E_ARG, "all four noise buffers are required");
+  if (given) {
+    if ((rc = want(io->d_rand_a, io->n_rand_a, N * A, "rand_a [N,A]"))) return rc;
+    if ((rc = want(io->d_rand_l, io->n_rand_l, 9 * B, "rand_l [B,3,3]"))) return rc;
+    if ((rc = want(io->d_rand_x1, io->n_rand_x1, 3 * N, "rand_x1 [N,3]"))) return rc;
+    if ((rc = want(io->d_rand_x2, io->n_rand_x2, 3 * N, "rand_x2 [N,3]"))) return rc;
+  }
+  return CHM_OK;
+}
+
+static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, float cond_scale, const chm_step_io* io,
+                       bool noise_required, bool noise_allowed, uint64_t seed, int64_t node_base, int64_t graph_base,
+                       hipStream_t s) {
   if (!b || !sc) return fail(CHM_E_ARG, "batch / schedule is NULL");
   if (b->P < 2) return fail(CHM_E_ARG, "sampling needs a batch created with max_pairs = 2");
   if (!b->m->film) return fail(CHM_E_ARG, "sampling needs a time-conditioned decoder (time_dim > 0)");
+  if (sc->T < 1) return fail(CHM_E_ARG, "schedule: T must be >= 1");
   if (!d_t && (t < 1 || t > sc->T)) return fail(CHM_E_ARG, "t out of range");
-  if (!d_a || !d_x || !d_l || !sc->d_coef || !sc->d_time_emb || !sc->d_q_one_step || !sc->d_q_mats)
-    return fail(CHM_E_ARG, "NULL state or schedule table");
-  if (b->m->d.text_dim > 0 && (!d_cond || !d_null)) return fail(CHM_E_ARG, "cond / null embeddings required");
-  if (ra && !(rl && rx1 && rx2)) return fail(CHM_E_ARG, "host noise: all four tensors or none");
+  if (!sc->d_coef || !sc->d_time_emb || !sc->d_q_one_step || !sc->d_q_mats)
+    return fail(CHM_E_ARG, "NULL schedule table");
+  if (sc->num_classes != b->m->d.max_atoms || sc->time_dim != b->m->d.time_dim)
+    return fail(CHM_E_ARG, "schedule: num_classes " + std::to_string(sc->num_classes) + " / time_dim " +
+                               std::to_string(sc->time_dim) + " do not match the model's " +
+                               std::to_string(b->m->d.max_atoms) + " / " + std::to_string(b->m->d.time_dim));
+  int rc = check_step_io(b, io, noise_required, noise_allowed);
+  if (rc) return rc;
+  const bool host_noise = io->d_rand_a != nullptr;
+  int64_t* d_a = io->d_atom_types;
+  float *d_x = io->d_frac, *d_l = io->d_lattices;
+  const float *d_cond = b->m->d.text_dim > 0 ? io->d_cond : nullptr, *d_null = b->m->d.text_dim > 0 ? io->d_null : nullptr;
   // time-embedding row: host t -> pointer offset; device t -> offset inside the kernel
   const float* temb = d_t ? sc->d_time_emb : sc->d_time_emb + (size_t)t * TD;
-  int rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 3, s);
+  rc = run_decoder(b, 2, d_a, d_x, d_l, temb, 0, d_t, d_cond, d_null, 3, s);
   if (rc) return rc;
   StepArgs sa;
   std::memset(&sa, 0, sizeof(sa));
@@ -1395,7 +1439,7 @@ static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, fl
   sa.cs_null = (float)(1.0 - (double)cond_scale); sa.cs_cond = cond_scale;
   sa.coef = sc->d_coef; sa.q_one_step = sc->d_q_one_step; sa.q_mats = sc->d_q_mats;
   sa.HO = b->HO; sa.LAT = b->LAT; sa.a = d_a; sa.x = d_x; sa.l = d_l; sa.n2g = b->n2g;
-  sa.ra = ra; sa.rl = rl; sa.rx1 = rx1; sa.rx2 = rx2;
+  if (host_noise) { sa.ra = io->d_rand_a; sa.rl = io->d_rand_l; sa.rx1 = io->d_rand_x1; sa.rx2 = io->d_rand_x2; }
   sa.seed = seed; sa.node_base = node_base; sa.graph_base = graph_base;
   HIPCHK(step_predictor(sa, s));
   // corrector: same t and text as the predictor, so its FiLM conditioning is reused
@@ -1406,36 +1450,36 @@ static int sample_step(chm_batch* b, const chm_schedule* sc, int t, int* d_t, fl
   return CHM_OK;
 }
 
-extern "C" int chm_sample_step(chm_batch* b, const chm_schedule* sc, int t, float cond_scale, int64_t* d_a, float* d_x,
-                               float* d_l, const float* d_cond, const float* d_null, const float* ra, const float* rl,
-                               const float* rx1, const float* rx2, uint64_t seed, int64_t node_base,
-                               int64_t graph_base, void* stream) {
-  return sample_step(b, sc, t, nullptr, cond_scale, d_a, d_x, d_l, d_cond, d_null, ra, rl, rx1, rx2, seed, node_base,
-                     graph_base, (hipStream_t)stream);
+extern "C" int chm_sample_step(chm_batch* b, const chm_schedule* sc, int t, float cond_scale, const chm_step_io* io,
+                               uint64_t seed, int64_t node_base, int64_t graph_base, void* stream) {
+  return sample_step(b, sc, t, nullptr, cond_scale, io, false, true, seed, node_base, graph_base, (hipStream_t)stream);
 }
 
-extern "C" int chm_sample_step_dt(chm_batch* b, const chm_schedule* sc, int32_t* d_t, float cond_scale, int64_t* d_a,
-                                  float* d_x, float* d_l, const float* d_cond, const float* d_null, uint64_t seed,
-                                  int64_t node_base, int64_t graph_base, void* stream) {
+extern "C" int chm_sample_step_dt(chm_batch* b, const chm_schedule* sc, int32_t* d_t, float cond_scale,
+                                  const chm_step_io* io, uint64_t seed, int64_t node_base, int64_t graph_base,
+                                  void* stream) {
   if (!d_t) return fail(CHM_E_ARG, "d_t is NULL");
-  return sample_step(b, sc, 0, d_t, cond_scale, d_a, d_x, d_l, d_cond, d_null, nullptr, nullptr, nullptr, nullptr,
-                     seed, node_base, graph_base, (hipStream_t)stream);
+  return sample_step(b, sc, 0, d_t, cond_scale, io, false, false, seed, node_base, graph_base, (hipStream_t)stream);
 }
 
 extern "C" int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sc, int32_t* d_t, float cond_scale,
-                                        int64_t* d_a, float* d_x, float* d_l, const float* d_cond, const float* d_null,
-                                        const float* ra, const float* rl, const float* rx1, const float* rx2,
-                                        void* stream) {
+                                        const chm_step_io* io, void* stream) {
   if (!d_t) return fail(CHM_E_ARG, "d_t is NULL");
-  if (!ra || !rl || !rx1 || !rx2) return fail(CHM_E_ARG, "all four noise buffers are required");
-  return sample_step(b, sc, 0, d_t, cond_scale, d_a, d_x, d_l, d_cond, d_null, ra, rl, rx1, rx2, 0, 0, 0,
-                     (hipStream_t)stream);
+  return sample_step(b, sc, 0, d_t, cond_scale, io, true, true, 0, 0, 0, (hipStream_t)stream);
 }
 
-extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, float* agg, void* stream) {
+extern "C" int chm_segment_mean(chm_batch* b, int pairs, const float* msg, int64_t msg_count, float* agg,
+                                int64_t agg_count, void* stream) {
   if (!b || !msg || !agg) return fail(CHM_E_ARG, "NULL argument");
   if (pairs < 1) return fail(CHM_E_ARG, "pairs must be >= 1");
   if (b->knn) return fail(CHM_E_UNSUPPORTED, "segment_mean: the fc edge layout only (knn edges change per call)");
+  const long H_ = b->m->d.hidden_dim;
+  if (msg_count != (int64_t)pairs * b->E * H_)
+    return fail(CHM_E_ARG, "msg: " + std::to_string(msg_count) + " elements, pairs x E x hidden_dim = " +
+                               std::to_string((int64_t)pairs * b->E * H_));
+  if (agg_count != (int64_t)pairs * b->N * H_)
+    return fail(CHM_E_ARG, "agg: " + std::to_string(agg_count) + " elements, pairs x N x hidden_dim = " +
+                               std::to_string((int64_t)pairs * b->N * H_));
   HIPCHK(segment_mean(msg, agg, b->n2g, b->node_off, b->edge_off, b->natoms, b->N, b->E, pairs, (hipStream_t)stream));
   return CHM_OK;
 }
@@ -1445,8 +1489,22 @@ extern "C" int chm_d3pm_sample(int N, int A, int T, const float* logits, const i
   if (N < 0 || A < 1 || A > 128 || T < 1) return fail(CHM_E_ARG, "bad sizes");
   if (N == 0) return CHM_OK;
   if (!logits || !xt || !tn || !noise || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
-  HIPCHK(d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, noise, q1, qm, out, 0, 0,
-                     (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  // the device range check: the first node with t outside [1, T] or x_t outside [0, A) (N = none)
+  int* d_bad = nullptr;
+  HIPCHK(hipMallocAsync((void**)&d_bad, sizeof(int), s));
+  int h_bad = N;
+  hipError_t e = hipMemsetAsync(d_bad, 0x7f, sizeof(int), s);  // (0x7f7f7f7f: above any node index)
+  if (e == hipSuccess)
+    e = d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, noise, q1, qm, out, 0, 0, s, d_bad);
+  if (e == hipSuccess) e = hipMemcpyAsync(&h_bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s);
+  const hipError_t ef = hipFreeAsync(d_bad, s);
+  if (e == hipSuccess) e = ef;
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(CHM_E_HIP, std::string("chm_d3pm_sample: ") + hipGetErrorString(e));
+  if (h_bad < N)
+    return fail(CHM_E_ARG, "d3pm_sample: node " + std::to_string(h_bad) + " has t outside [1, " + std::to_string(T) +
+                               "] or x_t outside [0, " + std::to_string(A) + ")");
   return CHM_OK;
 }
 

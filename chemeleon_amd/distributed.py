@@ -122,19 +122,37 @@ def _world(group):
 def _shared_conditioning(model, texts, B, cond, null, group):
     """Conditioning vectors [B, text_dim] on every rank: the text encoder (or the given vectors) on
     rank 0 only, then one broadcast of each (the north star's "computed once on host and
-    broadcast"). None for a model without text guidance."""
+    broadcast"). None for a model without text guidance.
+
+    Rank 0 validates the given vectors and computes the conditioning first, then broadcasts a status
+    flag: if it failed, EVERY rank raises (rank 0 its own error, the others a RuntimeError naming it),
+    so no rank is left blocked in a broadcast that never comes (the other ranks may not hold the
+    vectors at all: sample_distributed lets rank 0 alone pass them)."""
     if not model.text_guide:
         return None, None
     world, rank = _world(group)
     dev = model.device
+    d = model.hparams["text_dim"]
+    err = None
+    c = torch.zeros(B, d, device=dev)
+    n = torch.zeros(B, d, device=dev)
     if rank == 0 or world == 1:
-        c, n = model._conditioning(texts, B, cond, null)
-    else:  # receive buffers of the same shape (every rank knows B and text_dim)
-        d = model.hparams["text_dim"]
-        c = torch.zeros(B, d, device=dev)
-        n = torch.zeros(B, d, device=dev)
-    if cond is not None and cond.shape[0] not in (1, B):
-        raise ValueError(f"text_embeds has {cond.shape[0]} rows for {B} crystals")
+        try:
+            for name, v in (("text_embeds", cond), ("null_text_embeds", null)):
+                if v is not None and (v.dim() != 2 or v.shape[0] not in (1, B) or v.shape[1] != d):
+                    raise ValueError(f"{name} has shape {tuple(v.shape)}; expected [1 or {B}, {d}] for {B} crystals")
+            c, n = model._conditioning(texts, B, cond, null)
+        except Exception as e:  # noqa: BLE001 (re-raised below, after every rank has heard of it)
+            err = e
+    if world > 1:
+        flag = torch.tensor([0 if err is None else 1], device=dev, dtype=torch.int32)
+        dist.broadcast(flag, 0, group=group)
+        if int(flag.item()):
+            if err is not None:
+                raise err
+            raise RuntimeError("rank 0 failed to compute the text conditioning (see rank 0's error); every rank stops")
+    elif err is not None:
+        raise err
     return broadcast_conditioning(c, n, 0, group)
 
 
@@ -142,7 +160,8 @@ def _shared_conditioning(model, texts, B, cond, null, group):
 def sample_states_distributed(model, natoms: Sequence[int], texts=None, cond_scale: float = 2.0,
                               step_lr: float = 1e-5, *, noise: str = "torch", seed: int = 0, text_embeds=None,
                               null_text_embeds=None, group=None, init: Optional[Tuple] = None,
-                              every_step=False, graph: Optional[bool] = None):
+                              every_step=False, graph: Optional[bool] = None, t_stop: int = 0, lanes: int = 1,
+                              clone: bool = False, **unsupported):
     """Reverse loop over a GLOBAL crystal list, sharded across the ranks of `group`: yields
     (t, atom_types, frac_coords, lattices) of the WHOLE batch on every rank, for every t
     (every_step=True, one all-gather per step: the stream / return_trajectory case), for the t in
@@ -154,7 +173,14 @@ def sample_states_distributed(model, natoms: Sequence[int], texts=None, cond_sca
     keeps its own rows, so the gathered result is bit-identical to the single-process run for any
     rank count, provided every rank seeded its generator the same way (torch.manual_seed(s) before
     the call, as for the reference). noise="philox": device noise keyed by (seed, t, global index);
-    the initial noise comes from Generator(seed) at the global size."""
+    the initial noise comes from Generator(seed) at the global size.
+
+    t_stop / lanes / clone act as in Chemeleon.sample_states (the final gather is at t = t_stop); the
+    shard placement keywords of sample_states (node_base, graph_base, global_sizes) are computed here
+    from the global list and refused if passed (ValueError on every rank, before any collective)."""
+    if unsupported:
+        raise ValueError(f"{sorted(unsupported)}: not accepted when sampling over ranks (the shard offsets and "
+                         "global sizes are computed from the global crystal list)")
     world, rank = _world(group)
     natoms = [int(n) for n in natoms]
     # every rank holds the same list, so every rank raises here, before any collective
@@ -184,11 +210,14 @@ def sample_states_distributed(model, natoms: Sequence[int], texts=None, cond_sca
     natoms_all = [natoms[r0:r1] for r0, r1 in ranges]
     it = model.sample_states(local, None, cond_scale, step_lr, noise=noise, seed=seed, text_embeds=cond,
                              null_text_embeds=null, clone=False, node_base=node_base, graph_base=g0, init=init,
-                             global_sizes=(N, B) if noise == "torch" else None, graph=graph)
+                             global_sizes=(N, B) if noise == "torch" else None, graph=graph, t_stop=t_stop,
+                             lanes=lanes)
     want = None if isinstance(every_step, bool) else {int(t) for t in every_step}
     for t, a, x, lat in it:
-        if t == 0 or (every_step is True) or (want is not None and t in want):
+        if t == t_stop or (every_step is True) or (want is not None and t in want):
             A_, X_, L_, _ = gather_states((a, x, lat), local, group, natoms_all=natoms_all)
+            if clone and world == 1:  # (one rank: the gather hands back the sampler's own buffers)
+                A_, X_, L_ = A_.clone(), X_.clone(), L_.clone()
             yield t, A_, X_, L_
 
 

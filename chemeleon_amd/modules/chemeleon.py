@@ -272,7 +272,8 @@ class Chemeleon(nn.Module):
         temb_d = temb.float().to(dev).contiguous()
         q1 = self.d3pm.q_one_step_mats.to(dev).float().contiguous()
         qm = self.d3pm.q_mats.to(dev).float().contiguous()
-        sched = _lib.chm_schedule(T, coef_d.data_ptr(), temb_d.data_ptr(), q1.data_ptr(), qm.data_ptr())
+        sched = _lib.chm_schedule(T, int(q1.shape[1]), int(temb_d.shape[1]), 0, coef_d.data_ptr(), temb_d.data_ptr(),
+                                  q1.data_ptr(), qm.data_ptr())
         self._tables[key] = (sched, (coef_d, temb_d, q1, qm))
         return self._tables[key]
 
@@ -429,12 +430,12 @@ class Chemeleon(nn.Module):
                             st.wait_stream(side)
                         n0 = noff[g0]
                         bk = lane_batches[k]
-                        tx = cond.shape[1] * 4 * g0 if cond is not None else 0
+                        io = _lib.step_io(a, x, lat, cond, null, node0=n0, graph0=g0, nodes=noff[g1] - n0,
+                                          graphs=g1 - g0)
                         with torch.cuda.stream(st):
                             _lib.check(L.chm_sample_step_dt(
-                                bk.handle, sched, _lib.ptr(d_t, 4 * k), float(cond_scale), _lib.ptr(a, 8 * n0),
-                                _lib.ptr(x, 12 * n0), _lib.ptr(lat, 36 * g0), _lib.ptr(cond, tx), _lib.ptr(null, tx),
-                                seed, node_base + n0, graph_base + g0, _lib.stream_handle(dev)), "chm_sample_step_dt")
+                                bk.handle, sched, _lib.ptr(d_t, 4 * k), float(cond_scale), io, seed, node_base + n0,
+                                graph_base + g0, _lib.stream_handle(dev)), "chm_sample_step_dt")
                     for st in lane_streams:
                         side.wait_stream(st)
             torch.cuda.current_stream(dev).wait_stream(side)
@@ -448,9 +449,9 @@ class Chemeleon(nn.Module):
                 nz = tuple(z.to(dev) for z in step_noise.draw())
             else:
                 nz = (None, None, None, None)
-            _lib.check(L.chm_sample_step(batch.handle, sched, t, float(cond_scale), _lib.ptr(a), _lib.ptr(x),
-                                         _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null), *[_lib.ptr(z) for z in nz],
-                                         seed, node_base, graph_base, stream), "chm_sample_step")
+            io = _lib.step_io(a, x, lat, cond, null, nz)
+            _lib.check(L.chm_sample_step(batch.handle, sched, t, float(cond_scale), io, seed, node_base, graph_base,
+                                         stream), "chm_sample_step")
             yield (t - 1,) + emit(a, x, lat)
 
     def _replay_torch_noise(self, batch, sched, a, x, lat, cond, null, cond_scale, step_noise, T, t_stop, emit):
@@ -469,9 +470,8 @@ class Chemeleon(nn.Module):
         with torch.cuda.stream(side):
             with torch.cuda.graph(hg, stream=side):
                 _lib.check(L.chm_sample_step_dt_noise(
-                    batch.handle, sched, _lib.ptr(d_t), float(cond_scale), _lib.ptr(a), _lib.ptr(x), _lib.ptr(lat),
-                    _lib.ptr(cond), _lib.ptr(null), *[_lib.ptr(z) for z in dnz], _lib.stream_handle(dev)),
-                    "chm_sample_step_dt_noise")
+                    batch.handle, sched, _lib.ptr(d_t), float(cond_scale), _lib.step_io(a, x, lat, cond, null, dnz),
+                    _lib.stream_handle(dev)), "chm_sample_step_dt_noise")
         cur = torch.cuda.current_stream(dev)
         cur.wait_stream(side)
         d_t.fill_(T)
@@ -512,9 +512,8 @@ class Chemeleon(nn.Module):
         if noise is not None and [tuple(z.shape) for z in nz] != [(N, A), (B, 3, 3), (N, 3), (N, 3)]:
             raise ValueError(f"noise must be (rand_a [N,{A}], rand_l [B,3,3], rand_x1 [N,3], rand_x2 [N,3])")
         _lib.require_device(a, x, lat, cond, null, *nz)
-        _lib.check(_lib.load().chm_sample_step(batch.handle, sched, int(t), float(cond_scale), _lib.ptr(a),
-                                               _lib.ptr(x), _lib.ptr(lat), _lib.ptr(cond), _lib.ptr(null),
-                                               *[_lib.ptr(z) for z in nz], seed, node_base, graph_base,
+        _lib.check(_lib.load().chm_sample_step(batch.handle, sched, int(t), float(cond_scale),
+                                               _lib.step_io(a, x, lat, cond, null, nz), seed, node_base, graph_base,
                                                _lib.stream_handle(dev)),
                    "chm_sample_step")
         return a, x, lat

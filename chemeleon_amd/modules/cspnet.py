@@ -222,6 +222,8 @@ class CSPNet(nn.Module):
             _lib.check(_lib.load().chm_model_set_option(self.hip_model().handle, key.encode(), int(value)),
                        "chm_model_set_option")
             self._options[key] = int(value)
+            if key == "node_ps":  # (a batch carves the pre-split operand buffers only when created with it)
+                self._batches.clear()
 
     def set_math(self, mode: str):
         """'split16' (default), 'bf16x3' or 'f32' for the decoder GEMMs (see include/chemeleon_hip.h).

@@ -1,18 +1,22 @@
-"""torch.ops.chemeleon.* — the torch-op layer over the C ABI (csrc/torch_ops.cpp).
+"""torch.ops.chemeleon.* / torch.classes.chemeleon.* — the torch-op layer over the C ABI
+(csrc/torch_ops.cpp).
 
     from chemeleon_amd import ops
     ops.load()
-    types, lattice, coords, nodes = torch.ops.chemeleon.decoder_forward(ops.handle(batch), 2, ...)
+    model = ops.model(chemeleon.decoder)                   # torch.classes.chemeleon.Model
+    batch = torch.classes.chemeleon.Batch(model, [40] * 64, 2, False, 20)
+    sched = ops.schedule(chemeleon, step_lr=1e-5)          # torch.classes.chemeleon.Schedule
+    torch.ops.chemeleon.sample_step(batch, sched, t, 2.0, a, x, lat, cond, null, None, None, None, None, 0, 0, 0)
 
-The ops take the library's batch handle (`CSPNet.hip_batch(...).handle`) and schedule address
-(`Chemeleon.schedule_tables(...)[0]`), launch on the caller's current HIP stream, allocate outputs
-through the PyTorch caching allocator and raise RuntimeError (TORCH_CHECK) with chm_last_error() on a
-failing call. They are registered for the CUDA (= HIP) dispatch key only: CPU tensors raise
-NotImplementedError, there is no CPU fallback. The ctypes binding (chemeleon_amd._lib) reaches the same
-entry points; the sampler uses that one and the ops serve torch-native callers.
+The classes own the library's objects (reference-counted: a Batch holds its Model, a Schedule its
+tables), so TorchScript and C++ callers build and drive the sampler with no ctypes object in sight.
+The ops launch on the current HIP stream of the batch's device under a device guard for it, refuse
+tensors on any other device, allocate outputs through the PyTorch caching allocator and raise
+RuntimeError (TORCH_CHECK) with chm_last_error() on a failing call. They are registered for the CUDA
+(= HIP) dispatch key only: CPU tensors raise NotImplementedError, there is no CPU fallback. The sampler
+itself keeps the ctypes binding (chemeleon_amd._lib); both reach the same entry points.
 """
 
-import ctypes
 import os
 import threading
 
@@ -26,7 +30,8 @@ _loaded = False
 
 
 def load(path: str = None):
-    """Register torch.ops.chemeleon.* (once). Raises ImportError if the op library is missing."""
+    """Register torch.ops.chemeleon.* and torch.classes.chemeleon.* (once). Raises ImportError if the
+    op library is missing."""
     global _loaded
     with _lock:
         if _loaded:
@@ -41,15 +46,19 @@ def load(path: str = None):
         return torch.ops.chemeleon
 
 
-def handle(obj) -> int:
-    """The int the ops take for a batch: a HipBatch, its ctypes handle or an int."""
-    h = getattr(obj, "handle", obj)
-    h = getattr(h, "value", h)
-    if not h:
-        raise ValueError("null batch handle")
-    return int(h)
+def model(decoder, math: str = None):
+    """torch.classes.chemeleon.Model of a CSPNet's current weights (its state_dict order, the C ABI's)."""
+    load()
+    params = [p.detach().float().contiguous() for p in decoder.ordered_parameters()]
+    m = torch.classes.chemeleon.Model(params, decoder.hidden_dim, decoder.time_dim, decoder.text_dim,
+                                      decoder.num_layers, decoder.max_atoms, decoder.num_freqs)
+    if math is not None:
+        m.set_math(math)
+    return m
 
 
-def schedule_address(sched) -> int:
-    """The int the ops take for a chm_schedule (Chemeleon.schedule_tables(step_lr)[0])."""
-    return ctypes.addressof(sched)
+def schedule(chemeleon, step_lr: float = 1e-5):
+    """torch.classes.chemeleon.Schedule of a Chemeleon's per-timestep tables (schedule_tables)."""
+    load()
+    _, (coef, temb, q1, qm) = chemeleon.schedule_tables(step_lr)
+    return torch.classes.chemeleon.Schedule(coef, temb, q1, qm)

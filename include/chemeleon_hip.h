@@ -87,7 +87,8 @@ void chm_model_destroy(chm_model* m);
  *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag", "edge_layer_min": edge-layer
  *     schedules (bit-identical).
  *   "node_ps" (0 / 1): split16 node GEMMs read their A operands pre-split by the producing kernels (not
- *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs"). The persistent one-grid kernel (edge_layer_dyn) runs only where
+ *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs"); a batch carves their buffers only
+ *     when created while the option is set (batches created without it keep the in-loop split). The persistent one-grid kernel (edge_layer_dyn) runs only where
  *     model creation saw 8 XCDs ("xcd_mask" = 0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD
  *     exit, the launch's self-check must raise the repair), "edge_layer_repair", "edge_tail_timeout",
  *     "edge_tail_norepair" (WRONG results after a timeout), "edge_rows_nowait".
@@ -213,59 +214,96 @@ int chm_training_loss(chm_batch* b, const chm_train_tables* tt, const int64_t* d
  *   d_coef [T+1][8]: {c0, c1, sigma_l, step_x, std_x, sqrt(sigma_norm),
  *                     step_lr*(sigma_t/sigma_begin)^2, sqrt(2*that)}
  *   d_time_emb [T+1][time_dim]: SinusoidalTimeEmbeddings(t) (cspnet.py:21-35)
- *   d_q_one_step, d_q_mats [T+1][A][A]: D3PM buffers (diff_utils.py:168-185) */
+ *   d_q_one_step, d_q_mats [T+1][A][A]: D3PM buffers (diff_utils.py:168-185)
+ * num_classes (= A) and time_dim describe the tables; a step refuses a schedule
+ * whose num_classes / time_dim differ from its batch's model (CHM_E_ARG). */
 typedef struct {
   int T;
+  int num_classes;
+  int time_dim;
+  int reserved;
   const float* d_coef;
   const float* d_time_emb;
   const float* d_q_one_step;
   const float* d_q_mats;
 } chm_schedule;
 
+/* The device buffers of one reverse step, each with its ELEMENT count. Every count is
+ * checked against the batch (N nodes, B crystals) and its model (A = max_atoms classes,
+ * text_dim) before anything is enqueued: a mis-sized buffer returns CHM_E_ARG with
+ * chm_last_error() naming it, never an out-of-bounds access on the device.
+ *   d_atom_types [N] int64, d_frac [N,3], d_lattices [B,3,3]: the state, updated in place;
+ *   d_cond, d_null [B,text_dim]: conditioning vectors (NULL / 0 when text_dim = 0);
+ *   parity-mode noise, all four or none (NULL: device Philox noise):
+ *   d_rand_a [N,A] uniforms, d_rand_l [B,3,3], d_rand_x1 [N,3], d_rand_x2 [N,3] normals. */
+typedef struct chm_step_io {
+  int64_t* d_atom_types;
+  int64_t n_atom_types;
+  float* d_frac;
+  int64_t n_frac;
+  float* d_lattices;
+  int64_t n_lattices;
+  const float* d_cond;
+  int64_t n_cond;
+  const float* d_null;
+  int64_t n_null;
+  const float* d_rand_a;
+  int64_t n_rand_a;
+  const float* d_rand_l;
+  int64_t n_rand_l;
+  const float* d_rand_x1;
+  int64_t n_rand_x1;
+  const float* d_rand_x2;
+  int64_t n_rand_x2;
+} chm_step_io;
+
 /* One reverse-diffusion step t -> t-1 of Chemeleon._sample_generator
  * (chemeleon.py:379-466): predictor CFG pair, D3PM atom-type sampling
  * (diff_utils.py:307-329), DDPM lattice update (clip at t == T), VE
  * predictor half step, corrector CFG pair, Langevin corrector, wrap to [0,1).
- * State is updated in place: d_a [N] int64, d_x [N,3], d_l [B,3,3].
- * d_cond, d_null: [B,text_dim] conditioning vectors.
- * Noise: if d_rand_a != NULL the four host-drawn tensors of the reference's
- * RNG stream are used (parity mode): rand_a [N,A] uniform, rand_l [B,3,3],
- * rand_x1 [N,3], rand_x2 [N,3] normals; they are ignored at t == 1 as in the
- * reference. If d_rand_a == NULL, noise comes from a counter-based Philox
- * generator keyed by (seed, t, global node / graph index), so results do not
- * depend on how samples are sharded across GPUs. `node_base`/`graph_base`
- * are the global indices of this batch's first node / graph for that key. */
-int chm_sample_step(chm_batch* b, const chm_schedule* sched, int t, float cond_scale, int64_t* d_a, float* d_x,
-                    float* d_l, const float* d_cond, const float* d_null, const float* d_rand_a,
-                    const float* d_rand_l, const float* d_rand_x1, const float* d_rand_x2, uint64_t seed,
-                    int64_t node_base, int64_t graph_base, void* stream);
+ * Buffers: `io` (state updated in place). With the four noise buffers the
+ * host-drawn tensors of the reference's RNG stream are used (parity mode;
+ * ignored at t == 1 as in the reference); without them noise comes from a
+ * counter-based Philox generator keyed by (seed, t, global node / graph
+ * index), so results do not depend on how samples are sharded across GPUs.
+ * `node_base`/`graph_base` are the global indices of this batch's first
+ * node / graph for that key. */
+int chm_sample_step(chm_batch* b, const chm_schedule* sched, int t, float cond_scale, const chm_step_io* io,
+                    uint64_t seed, int64_t node_base, int64_t graph_base, void* stream);
 
 /* Graph-capturable form of chm_sample_step: t is read from device memory
  * (*d_t, int32) and decremented by the step's last kernel, so one captured
  * step (hipStreamBeginCapture ... hipGraphLaunch) replayed T times walks
- * t = T .. 1. Noise comes from the counter-based Philox generator only. */
-int chm_sample_step_dt(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale, int64_t* d_a,
-                       float* d_x, float* d_l, const float* d_cond, const float* d_null, uint64_t seed,
-                       int64_t node_base, int64_t graph_base, void* stream);
+ * t = T .. 1. Noise comes from the counter-based Philox generator only (the
+ * noise buffers of `io` must be NULL). */
+int chm_sample_step_dt(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale, const chm_step_io* io,
+                       uint64_t seed, int64_t node_base, int64_t graph_base, void* stream);
 
-/* The same with the noise read from fixed device buffers (d_rand_* as in chm_sample_step, all four):
- * the caller refills them before every replay (the reference's CPU RNG stream drawn on the host and
+/* The same with the noise read from the four fixed device buffers of `io` (required): the
+ * caller refills them before every replay (the reference's CPU RNG stream drawn on the host and
  * copied in stream order), so parity-mode sampling also runs as one captured step. At t == 1 the
  * buffers are not read (their stale contents are finite uniforms / normals). */
-int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale, int64_t* d_a,
-                             float* d_x, float* d_l, const float* d_cond, const float* d_null, const float* d_rand_a,
-                             const float* d_rand_l, const float* d_rand_x1, const float* d_rand_x2, void* stream);
+int chm_sample_step_dt_noise(chm_batch* b, const chm_schedule* sched, int32_t* d_t, float cond_scale,
+                             const chm_step_io* io, void* stream);
 
 /* Standalone message-passing aggregation (scatter_mean of edge messages onto
  * their source node; chemeleon/utils/scatter.py:88-112 as called from
  * cspnet.py:155-160) over this batch's fc edge layout:
- *   d_msg [pairs,E,H] -> d_agg [pairs,N,H], agg[i] = sum_j msg[(i,j)] / max(n_g,1),
- * H = hidden_dim (512); fc batches only (CHM_E_UNSUPPORTED for knn). */
-int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, float* d_agg, void* stream);
+ *   d_msg [pairs,E,H] (msg_count elements) -> d_agg [pairs,N,H] (agg_count elements),
+ *   agg[i] = sum_j msg[(i,j)] / max(n_g,1), H = hidden_dim (512); the counts must be
+ * exactly pairs*E*H and pairs*N*H (CHM_E_ARG otherwise); fc batches only
+ * (CHM_E_UNSUPPORTED for knn). */
+int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, int64_t msg_count, float* d_agg, int64_t agg_count,
+                     void* stream);
 
 /* D3PM reverse sampling for explicit inputs (diff_utils.py:307-329):
  * d_logits [N,A], d_xt [N] int64, d_t [N] int64 per-node timestep,
- * d_noise [N,A] uniform -> d_out [N] int64. Tables as in chm_schedule. */
+ * d_noise [N,A] uniform -> d_out [N] int64. Tables as in chm_schedule.
+ * Every t must lie in [1, T] and every x_t in [0, A) (the reference indexes its
+ * tables with them and raises otherwise): the kernel checks them on the device,
+ * and an out-of-range index makes the call return CHM_E_ARG with chm_last_error()
+ * naming the first offending node (its d_out entry is -1). The check needs the
+ * result, so this entry point synchronises `stream` before returning. */
 int chm_d3pm_sample(int N, int A, int T, const float* d_logits, const int64_t* d_xt, const int64_t* d_t,
                     const float* d_noise, const float* d_q_one_step, const float* d_q_mats, int64_t* d_out,
                     void* stream);
@@ -368,6 +406,10 @@ int64_t chm_batch_num_edges(const chm_batch* b);
  * knn-edge batch. Callers that allocate outputs or validate shapes use it (the torch-op layer,
  * chemeleon_amd/csrc/torch_ops.cpp, checks every tensor against it before a launch). */
 int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn);
+/* The HIP device ordinal the batch (and its model) lives on: every buffer passed with the batch
+ * must be memory of that device (the torch-op layer checks each tensor's device against it and
+ * launches under a device guard for it). Negative CHM_E_ARG for a NULL batch. */
+int chm_batch_device(const chm_batch* b);
 
 #ifdef __cplusplus
 }

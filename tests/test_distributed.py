@@ -105,11 +105,11 @@ class _StubModel:
         return cond.expand(B, -1).contiguous(), null.expand(B, -1).contiguous()
 
     def sample_states(self, natoms, texts, cond_scale, step_lr, *, noise, seed, text_embeds, null_text_embeds, clone,
-                      node_base, graph_base, init, global_sizes, graph):
+                      node_base, graph_base, init, global_sizes, graph, t_stop=0, lanes=1):
         self.calls.append(dict(natoms=list(natoms), node_base=node_base, graph_base=graph_base,
-                               global_sizes=global_sizes, cond=text_embeds.clone(), noise=noise))
+                               global_sizes=global_sizes, cond=text_embeds.clone(), noise=noise, lanes=lanes))
         N, B = sum(natoms), len(natoms)
-        for t in range(3, -1, -1):
+        for t in range(3, t_stop - 1, -1):
             a = torch.arange(node_base, node_base + N) * 10 + t
             x = torch.arange(node_base, node_base + N, dtype=torch.float32)[:, None].repeat(1, 3) + t
             lat = torch.arange(graph_base, graph_base + B, dtype=torch.float32)[:, None, None].repeat(1, 3, 3) + t
@@ -162,3 +162,56 @@ def test_distributed_sampler_gathers_the_whole_batch_on_every_rank():
         g0 = parts[rank][0]
         assert gsz == (sum(nat), len(nat)) and gb == g0 and nb == sum(nat[:g0])
         assert cond == [3.0] * (parts[rank][1] - g0)
+
+
+def _error_worker(rank, world, port, q):
+    """Rank 0 alone holds (mis-shaped) conditioning; an unsupported keyword; t_stop / lanes forwarded."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from chemeleon_amd.distributed import sample_states_distributed
+        nat = [3, 5, 2, 7]
+        m = _StubModel()
+        out = {}
+        bad = torch.full((3, 4), 1.0) if rank == 0 else None  # 3 rows for 4 crystals: only rank 0 can tell
+        try:
+            list(sample_states_distributed(m, nat, None, noise="torch", text_embeds=bad, null_text_embeds=bad))
+            out["shape"] = "no error"
+        except ValueError as e:
+            out["shape"] = "ValueError" if "text_embeds has shape" in str(e) else repr(e)
+        except RuntimeError as e:
+            out["shape"] = "RuntimeError" if "rank 0 failed" in str(e) else repr(e)
+        try:
+            list(sample_states_distributed(m, nat, None, noise="torch", text_embeds=torch.ones(1, 4),
+                                           null_text_embeds=torch.ones(1, 4), node_base=5))
+            out["kw"] = "no error"
+        except ValueError as e:
+            out["kw"] = "ValueError" if "node_base" in str(e) else repr(e)
+        ts = [t for t, *_ in sample_states_distributed(m, nat, None, noise="torch", text_embeds=torch.ones(1, 4),
+                                                         null_text_embeds=torch.ones(1, 4), t_stop=2, lanes=2)]
+        out["t_stop"] = ts
+        out["lanes"] = m.calls[-1]["lanes"]
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_sampler_errors_reach_every_rank():
+    """a conditioning error found on rank 0 (the only rank holding the vectors) raises on EVERY
+    rank instead of leaving the others blocked in the broadcast; sample_states keywords the shards compute
+    themselves are refused on every rank before any collective; t_stop and lanes are forwarded."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_error_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0]["shape"] == "ValueError" and res[1]["shape"] == "RuntimeError"
+    for r in (0, 1):
+        assert res[r]["kw"] == "ValueError"
+        assert res[r]["t_stop"] == [2]
+        assert res[r]["lanes"] == 2

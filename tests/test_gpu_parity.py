@@ -127,7 +127,7 @@ def test_segment_mean_matches_oracle(model1000):
     msg = torch.randn(2, b.num_edges, 512, generator=gen)
     agg = torch.empty(2, b.num_nodes, 512, device=DEV)
     md = msg.to(DEV)
-    _lib.check(_lib.load().chm_segment_mean(b.handle, 2, _lib.ptr(md), _lib.ptr(agg), _lib.stream_handle()), "sm")
+    _lib.check(_lib.load().chm_segment_mean(b.handle, 2, _lib.ptr(md), md.numel(), _lib.ptr(agg), agg.numel(), _lib.stream_handle()), "sm")
     e = O.fc_edges(nat)
     for c in range(2):
         ref = O.scatter_mean(msg[c], e[0], b.num_nodes)
