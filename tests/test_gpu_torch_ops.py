@@ -212,14 +212,17 @@ def test_ops_check_shapes_and_devices_before_launch(model, chem, tmodel):
         chem.sample_step(b, sched, 10, 2.0, a, x, lat, c[:1], c, None, None, None, None, 0, 0, 0)
     with pytest.raises(RuntimeError, match="t must be in"):
         chem.sample_step(b, sched, sched.num_timesteps() + 1, 2.0, a, x, lat, c, c, None, None, None, None, 0, 0, 0)
-    # a tensor on another device than the batch's (a CPU tensor beside HIP ones: the op is dispatched to the
-    # HIP kernel by the others and must refuse it, as it refuses one on another GPU)
-    with pytest.raises(RuntimeError, match="cond is on cpu"):
+    # a tensor on another device than the batch's: a CPU tensor beside HIP ones (the op is dispatched to the
+    # HIP kernel by the others and must refuse it) and, where a second GPU exists, a tensor on that GPU
+    with pytest.raises(RuntimeError, match="cond: chemeleon ops run on a HIP device only"):
         chem.sample_step(b, sched, 10, 2.0, a, x, lat, c.cpu(), c, None, None, None, None, 0, 0, 0)
-    with pytest.raises(RuntimeError, match="text is on cpu"):
+    with pytest.raises(RuntimeError, match="text: chemeleon ops run on a HIP device only"):
         chem.decoder_forward(b, 1, a, x, lat, te, tx.cpu())
-    with pytest.raises(RuntimeError, match="frac is on cpu"):
+    with pytest.raises(RuntimeError, match="frac: chemeleon ops run on a HIP device only"):
         chem.decoder_forward(b, 1, a, x.cpu(), lat, te, tx)
+    if torch.cuda.device_count() > 1:
+        with pytest.raises(RuntimeError, match="cond is on cuda:1, the batch on cuda:0"):
+            chem.sample_step(b, sched, 10, 2.0, a, x, lat, c.to("cuda:1"), c, None, None, None, None, 0, 0, 0)
     # a schedule of another class count
     T1 = sched.num_timesteps() + 1
     other = torch.classes.chemeleon.Schedule(torch.zeros(T1, 8, device=DEV), torch.zeros(T1, 128, device=DEV),
