@@ -49,14 +49,7 @@ struct GemmArgs {
   const int* natoms; const int* n2g;
   float* agg;                             // [P][N][H]
   int linear_order;                       // node_gemm: 1 = tiles in launch order (A/B only), 0 = XCD-aware
-  // split16 node GEMMs (not pre-split): the K loop accumulates kNodeSeg segments of K/kNodeSeg each from zero
-  // and adds them in segment order, whatever the split, so ksplits = 1, 2 or 4 give the same bits. ksplits > 1
-  // (short grids): block (tile, split) computes K/ksplits of the tile and stores its segments' sums to
-  // part; the tile's last block (tile_cnt) adds all segments in order and runs the epilogue. part holds
-  // kNodeSeg x (tiles x 64 x 128... the tile's elements) floats per tile, tile_cnt one zeroed word per tile.
-  int ksplits; float* part; unsigned* tile_cnt;
 };
-constexpr int kNodeSeg = 4;
 
 enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 
@@ -195,7 +188,6 @@ hipError_t node_gemm_init();
 extern int g_node_variant;  // microbenchmark probes of node_gemm (0 in the product)
 extern int g_node_blocks;   // S16 node GEMM blocks per CU override (microbenchmarks; 0 = default)
 extern int g_node_rows;     // S16 node GEMM tile rows override (microbenchmarks; 0 = default, 64, 128)
-extern int g_node_ksplit;   // S16 node GEMM K-split override (microbenchmarks; 0 = default, 1, 2, 4)
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);
 extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)

@@ -178,26 +178,14 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
   const int ntn = g.N / NN;
-  // SEG (split16, A split in the loop): the K loop runs kNodeSeg segments, each accumulated from zero and
-  // added to the total in segment order, so a K split over ks blocks (short grids: a block's K loop is
-  // one latency chain) gives the same bits as one block (GemmArgs::ksplits)
-  constexpr bool SEG = S16 && !PS;
-  constexpr bool SPLITK = SEG && NMT == 64;  // (K splits on the short-grid tiling only: the 128-row tiles keep
-                                             // their registers for the accumulators and the segment total)
-  const int ks = SPLITK && g.ksplits > 1 ? g.ksplits : 1;
-  const long ntile = (long)gridDim.x / ks;
-  const int kpart = ks > 1 ? (int)(blockIdx.x % ks) : 0;  // (a tile's K parts are consecutive blocks)
-  const long bt = ks > 1 ? (long)blockIdx.x / ks : (long)blockIdx.x;
   // XCD-aware order (workgroups go round-robin to the 8 XCDs): each XCD takes a contiguous range of
   // tiles, so the column tiles of a row tile run on one XCD and read their A rows once from HBM
   // (without it every column tile fetched A again into another XCD's L2: 538 MB per launch vs 84-168)
-  const long bid = g.linear_order || ks > 1 ? bt : xcd_remap(bt, ntile);
+  const long bid = g.linear_order ? (long)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int n0 = (int)(bid % ntn) * NN;
   const long row0 = (bid / ntn) * NM;
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
   const int nk = g.K / NK;
-  const int seglen = nk / kNodeSeg;                    // K-tiles per segment (even: K % 128 == 0, host-checked)
-  const int tb = kpart * (nk / ks), te = tb + nk / ks;  // this block's K-tiles
 
   // ---- glds sources. A: instruction q (of 8, or 4 for 64 rows) covers rows 16q + (L >> 2), LDS
   // piece L & 3 holding logical piece (L & 3) ^ ((L >> 4) & 3); wave w issues q = NI w .. NI w + NI-1.
@@ -236,7 +224,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     }
   }
   auto issue = [&](int t) {
-    const int k0 = (t < te ? t : te - 1) * NK;  // past the end: re-read the last tile into an idle stage
+    const int k0 = (t < nk ? t : nk - 1) * NK;  // past the end: re-read the last tile into an idle stage
     char* st = lds + (t % NST_) * STB_;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
@@ -249,46 +237,12 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   };
 
   f32x16 acc[NI][2];
-  f32x16 tot[NI][2];  // SEG, one block per tile: the sum of the finished segments
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
-  // segment `seg` done: into the total (one block per tile) or, split tiles, to the partial-sum buffer as
-  // 8-byte agent-scope stores (written through to memory: the tile's last block may run on another XCD;
-  // MI355X_MICROARCH.md hand-off table, first row); the accumulators restart from zero
-  constexpr int NPAIR = NI * 2 * 8;  // 8-byte pairs of this thread's accumulators
-  unsigned long long* part = reinterpret_cast<unsigned long long*>(g.part) + bid * (long)kNodeSeg * NPAIR * 256;
-  auto fold = [&](int seg) __attribute__((always_inline)) {
-    if constexpr (SEG) {
-      if (SPLITK && ks > 1) {
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              const int e = (i * 2 + j) * 8 + r / 2;
-              const unsigned long long v = (unsigned long long)__float_as_uint(acc[i][j][r]) |
-                                           ((unsigned long long)__float_as_uint(acc[i][j][r + 1]) << 32);
-              __hip_atomic_store(part + ((long)seg * NPAIR + e) * 256 + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) tot[i][j] += acc[i][j];
-      }
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-    }
-  };
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   // fragment offsets: A row wm*NM/2 + 32i + r32 pieces 2h, 2h+1; W row wn*64 + 32j + r32 piece h
   const int asw = (r32 >> 2) & 3, wsw = (r32 >> 3) & 1;
@@ -407,18 +361,15 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
         }
   };
 #pragma unroll
-  for (int t = 0; t < AHEAD; ++t) issue(tb + t);
-  vm_wait<(AHEAD - 1) * GL>();  // tile tb has landed
+  for (int t = 0; t < AHEAD; ++t) issue(t);
+  vm_wait<(AHEAD - 1) * GL>();  // tile 0 has landed
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  read_raw(tb, 0);
+  read_raw(0, 0);
   __builtin_amdgcn_s_waitcnt(0xC07F);
   split(0);
   auto step = [&](int t, auto CUR) {
     constexpr int cur = decltype(CUR)::value;
-    if constexpr (SEG && cur == 0) {  // tile t opens segment t / seglen: the previous one is complete
-      if (t != tb && t % seglen == 0) fold(t / seglen - 1);
-    }
     if constexpr (PS) {  // tile t opens a new 128-column chunk of A: move the accumulators to its scale
       if (t > 0 && (t & 7) == 0) {
         const int c = t >> 3;
@@ -472,53 +423,11 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     }
     __builtin_amdgcn_s_setprio(0);
   };
-  for (int t = tb; t < te; t += 2) {  // nk = K / 16 is even for every node GEMM (K = 512, 640, 1024)
+  for (int t = 0; t < nk; t += 2) {  // nk = K / 16 is even for every node GEMM (K = 512, 640, 1024)
     step(t, std::integral_constant<int, 0>{});
     step(t + 1, std::integral_constant<int, 1>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-reads land before the block exits
-  if constexpr (SEG) {
-    fold(te / seglen - 1);
-    if (!SPLITK || ks == 1) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
-    } else if constexpr (SPLITK) {
-      // every wave's partial stores are done, then one lane counts this block; the tile's last block
-      // (its add returns ks - 1) adds the kNodeSeg segments in order and runs the epilogue
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      unsigned* flag = reinterpret_cast<unsigned*>(lds);
-      if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add(g.tile_cnt + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = old == (unsigned)(ks - 1);
-        if (last) __hip_atomic_store(g.tile_cnt + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (next launch)
-        *flag = last ? 1u : 0u;
-      }
-      __syncthreads();
-      if (*flag == 0u) return;
-#pragma unroll 1
-      for (int seg = 0; seg < kNodeSeg; ++seg)  // (one segment's loads in flight at a time: registers)
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              const int e = (i * 2 + j) * 8 + r / 2;
-              const unsigned long long v =
-                  __hip_atomic_load(part + ((long)seg * NPAIR + e) * 256 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              tot[i][j][r] += __uint_as_float((unsigned)v);
-              tot[i][j][r + 1] += __uint_as_float((unsigned)(v >> 32));
-            }
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
-      __syncthreads();  // (the flag word's LDS is reused by the epilogue)
-    }
-  }
 
   // lane l owns output row wm*NM/2 + 32i + (l & 31) and, per 4-register group q, the four
   // consecutive columns wn*64 + 32j + 8q + 4h .. +3
@@ -590,7 +499,6 @@ hipError_t node_gemm_init() {
 }
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
-int g_node_ksplit = 0;  // S16 K-split override (microbenchmarks, A/B): 0 = default, 1, 2 or 4
 int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
@@ -604,26 +512,12 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   if ((g.lda | g.lda2 | g.ldc) % 4) return hipErrorInvalidValue;  // 16-B aligned rows
   if (hipError_t e = node_gemm_init(); e != hipSuccess) return e;
   const long blocks = ((g.M + 127) / 128) * (g.N / NN);
-  dim3 grid((unsigned)blocks), block(256);
+  const dim3 grid((unsigned)blocks), block(256);
   const bool v1 = g_node_variant == 1;
   // S16, grids short of one 128-row block per CU: 64-row tiles (twice the blocks; M = 5120: 23 vs
   // 26 us at K = 512); above that 128-row tiles at three blocks per CU (M = 20480: 54 vs 65 us with
   // two), profiles/r2/node/node64_micro.log
   const int rows = g_node_rows ? g_node_rows : (blocks < 256 ? 64 : 128);
-  if (g.wscale && !g.aex) {
-    // split16 with the A split in the loop: segmented K accumulation (GemmArgs::ksplits), and on short grids the
-    // K loop split over up to 4 blocks per tile (each a quarter of the latency chain), bit-identical
-    if (g.K % (kNodeSeg * 2 * NK)) return hipErrorInvalidValue;
-    const long tiles = ((g.M + rows - 1) / rows) * (g.N / NN);
-    int ks = 1;
-    if (g.part && g.tile_cnt && rows == 64)  // (the 64-row tiling only: k_node_gemm's SPLITK)
-      ks = g_node_ksplit ? g_node_ksplit : tiles <= 400 ? 4 : tiles <= 800 ? 2 : 1;
-    if (ks != 1 && ks != 2 && ks != 4) return hipErrorInvalidValue;
-    g.ksplits = ks;
-    if (ks > 1) grid = dim3((unsigned)(tiles * ks));
-  } else {
-    g.ksplits = 1;
-  }
   if (g.aex) {  // pre-split A (split16 only)
     if (!g.wscale || g.K % 128 || g.ksplit % 128 || (g.Cs && (g.N % 128 || !g.cex))) return hipErrorInvalidValue;
     const int nb = g_node_blocks ? g_node_blocks : 3;
@@ -641,16 +535,16 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
     return hipGetLastError();
   }
   if (g.wscale && rows == 64) {
-    const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN) * g.ksplits));
+    const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
     if (g_node_blocks == 4)
       hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 4, 64> : k_node_gemm<0, true, 4, 64>), grid64, block, LDS64_4, s, g);
     else
       hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3, 64> : k_node_gemm<0, true, 3, 64>), grid64, block, LDS64_3, s, g);
     return hipGetLastError();
   }
-  // S16: two blocks per CU (4 stages each). (Three blocks with 3 stages ran 7% faster at M = 40960 before the
-  // segmented accumulation, whose segment total does not fit their 168 registers.)
-  const int nb = g_node_blocks ? g_node_blocks : 2;
+  // S16: three blocks per CU (3 stages each): more waves to hide the K-loop latency (-7% at
+  // M = 40960, -17% at M = 20480 against two blocks with 5 stages)
+  const int nb = g_node_blocks ? g_node_blocks : 3;
   if (g.wscale && nb == 3)
     hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3> : k_node_gemm<0, true, 3>), grid, block, LDS3, s, g);
   else if (g.wscale)

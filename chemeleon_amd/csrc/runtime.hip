@@ -56,11 +56,7 @@ constexpr int kMaxLag = 1000;
 // the persistent one-grid kernel from this many row tiles on (same-box A/B, profiles/r3/ab_*: 512x40 (3200)
 // 60.2 -> 59.2 ms per step; 64x40 (400) 8.34 -> 8.44: the per-job atomic costs more than the XCD
 // balancing gains in a short grid)
-constexpr long kDynMinTiles = 1024;
-// node GEMMs may split their K loop (node_gemm.hip) on batches of at most this many node rows P * N (the
-// per-GPU shares of the multi-GPU runs and configs[1]: 64x40 is 5120 rows); the partial-sum buffer costs
-// 128 KB per 64-row x 128-column tile of the widest node GEMM (N = 1024): 80 MB at 5120 rows
-constexpr long kNodeSplitRows = 16384;  // edge_lag's upper bound (sizes the persistent one-grid kernel's row slots)
+constexpr long kDynMinTiles = 1024;  // edge_lag's upper bound (sizes the persistent one-grid kernel's row slots)
 
 struct chm_model {
   chm_dims d;
@@ -133,11 +129,6 @@ struct chm_batch {
   void *Hs, *Hls, *aggs, *Us;
   int *He, *Hle, *agge, *Ue;
   unsigned* rowmax;  // split16: per S row, the packed int8 exponents of its four 128-column chunks, [P][E]
-  // split16 node GEMMs on short grids (P * N <= kNodeSplitRows): the K loop split over up to 4 blocks per
-  // 64-row tile (GemmArgs::ksplits): per tile kNodeSeg segment sums (partial) and one arrival counter (zeroed
-  // at creation, returned to 0 by each tile's last block); null on larger batches (one block per tile)
-  float* npart = nullptr;
-  unsigned* ncnt = nullptr;
   void* owned = nullptr;  // the library's own allocation (chm_batch_create); null for caller workspaces
   size_t bytes = 0;
   // edge layer 1's partial last round (split16 / k_edge16, see run_decoder): rows [0, l1_rows_a) fill
@@ -762,14 +753,6 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->Hs = b->Hls = b->aggs = b->Us = nullptr;
     b->He = b->Hle = b->agge = b->Ue = nullptr;
   }
-  if (b->math == MATH_SPLIT16 && (long)P * N <= kNodeSplitRows) {
-    const long tiles = ((long)P * N + 63) / 64 * (2 * H / 128);
-    b->npart = fl((size_t)tiles * kNodeSeg * 16 * 256 * 2);  // (16 8-byte pairs per thread and segment)
-    b->ncnt = (unsigned*)carve((size_t)tiles * sizeof(unsigned));
-  } else {
-    b->npart = nullptr;
-    b->ncnt = nullptr;
-  }
   b->tail_flags = (unsigned*)carve(kMaxTailTiles * sizeof(unsigned));
   b->Hf = fl((size_t)P * N * H);
   b->HO = fl((size_t)P * N * HEADS_N);
@@ -859,8 +842,6 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
     if (e == hipSuccess && b->lflags) e = hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s);
   }
-  if (e == hipSuccess && b->ncnt)  // (node GEMM tile counters: each tile's last block returns its word to 0)
-    e = hipMemsetAsync(b->ncnt, 0, ((long)b->P * b->N + 63) / 64 * (2 * H / 128) * sizeof(unsigned), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     chm_batch_destroy(b);
@@ -1077,7 +1058,6 @@ static hipError_t run_gemm(const chm_batch* b, GemmArgs g, int epi, const void* 
   if (b->math == MATH_F32) return gemm(g, epi, s);
   if (b->math == MATH_SPLIT16 && W16 && (g.amax || g.aex) && b->m->node16 && b->m->node_glds && epi == EPI_STD) {
     g.Wp3 = W16; g.wscale = wsc;
-    g.part = b->npart; g.tile_cnt = b->ncnt;  // (short grids: the K loop split over blocks)
     return node_gemm(g, s);
   }
   g.Wp3 = W3;

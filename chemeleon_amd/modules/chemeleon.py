@@ -456,21 +456,20 @@ class Chemeleon(nn.Module):
 
     def _replay_torch_noise(self, batch, sched, a, x, lat, cond, null, cond_scale, step_noise, T, t_stop, emit):
         """Parity-mode noise (the reference's CPU RNG stream, this shard's rows of it) under a captured
-        reverse step, with the upload off the critical path.
+        reverse step, with no copy on the device's critical path.
 
-        Two device noise sets and two captured graphs of the same step (graph k reads set k), used on
-        alternate timesteps. Step t's draws go host -> pinned set k -> device set k on a copy stream, which
-        first waits for the replay that last read device set k (two steps earlier); the compute stream
-        waits only for that copy's event before replaying graph k. So the copy for step t runs while step
-        t+1 replays, the host draw for step t-1 runs while step t replays, and the compute stream sees no
-        copy in front of its replays. Bit-identical to eager stepping (test_torch_noise_graph_matches_eager):
-        the same draws reach the same kernels."""
+        Two pinned host noise sets and two captured graphs of the same step: graph k reads set k in place
+        (pinned host memory is mapped into the device's address space; the step kernels read each value
+        once, coalesced), and the graphs alternate over the timesteps. The host draws step t's noise into
+        set t & 1 while step t+1 replays, after waiting for the replay that last read that set (two steps
+        earlier), so the compute stream never waits for a copy and the draw hides under the replays.
+        Bit-identical to eager stepping (test_torch_noise_graph_matches_eager): the same draws reach the
+        same kernels."""
         dev = self.device
         L = _lib.load()
         d_t = torch.full((1,), T, dtype=torch.int32, device=dev)
         shapes = step_noise.local_shapes
-        dnz = [[torch.zeros(sh, dtype=torch.float32, device=dev) for sh in shapes] for _ in range(2)]
-        pin = [[torch.empty(sh, dtype=torch.float32).pin_memory() for sh in shapes] for _ in range(2)]
+        pin = [[torch.zeros(sh, dtype=torch.float32).pin_memory() for sh in shapes] for _ in range(2)]
         graphs = [torch.cuda.CUDAGraph() for _ in range(2)]
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -479,29 +478,18 @@ class Chemeleon(nn.Module):
                 with torch.cuda.graph(graphs[k], stream=side):
                     _lib.check(L.chm_sample_step_dt_noise(
                         batch.handle, sched, _lib.ptr(d_t), float(cond_scale),
-                        _lib.step_io(a, x, lat, cond, null, dnz[k]), _lib.stream_handle(dev)),
+                        _lib.step_io(a, x, lat, cond, null, pin[k]), _lib.stream_handle(dev)),
                         "chm_sample_step_dt_noise")
         cur = torch.cuda.current_stream(dev)
         cur.wait_stream(side)
-        copy = torch.cuda.Stream(device=dev)
-        copy.wait_stream(cur)
-        copied = [None, None]   # copy of pinned set k -> device set k done (host may refill pin[k]; replay k may run)
-        replayed = [None, None]  # the replay that read device set k done (the next copy into it may start)
+        replayed = [None, None]  # the replay that read set k done: the host may draw into it again
         d_t.fill_(T)
         for t in range(T, t_stop, -1):
             k = t & 1
             if t > 1:  # chemeleon.py:400-404, 418, 435, 455 (none at t = 1)
-                if copied[k] is not None:
-                    copied[k].synchronize()  # the copy out of pinned set k (two steps ago) is done
+                if replayed[k] is not None:
+                    replayed[k].synchronize()
                 step_noise.draw(out=pin[k])
-                with torch.cuda.stream(copy):
-                    if replayed[k] is not None:
-                        copy.wait_event(replayed[k])
-                    for dz, pz in zip(dnz[k], pin[k]):
-                        dz.copy_(pz, non_blocking=True)
-                    copied[k] = torch.cuda.Event()
-                    copied[k].record(copy)
-                cur.wait_event(copied[k])
             graphs[k].replay()
             replayed[k] = torch.cuda.Event()
             replayed[k].record(cur)

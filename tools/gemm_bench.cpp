@@ -169,37 +169,6 @@ int main(int argc, char** argv) {
     printf("empty kernel, 160 blocks: %.2f us per launch\n", te * 1e3);
     return 0;
   }
-  if (argc > 3 && std::string(argv[3]) == "nodesplit") {  // split16 node GEMM: K split over 1, 2, 4 blocks per tile
-    CK(node_gemm_init());
-    void* W16; float* wsc16; float* amax; float* part; unsigned* cnt;
-    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
-    const long tiles64 = (M + 63) / 64 * (N / 128);
-    CK(hipMalloc(&part, tiles64 * kNodeSeg * 16 * 256 * 8)); CK(hipMalloc(&cnt, tiles64 * 4));
-    CK(hipMemset(cnt, 0, tiles64 * 4));
-    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
-    std::vector<float> one(M, 1.0f);
-    CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
-    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax; g16.part = part; g16.tile_cnt = cnt;
-    const size_t nc = (size_t)M * N;
-    std::vector<float> c0(nc), c1(nc);
-    g_node_ksplit = 1;
-    CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(c0.data(), C, nc * 4, hipMemcpyDeviceToHost));
-    const int cfg[][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 4}, {64, 1}, {64, 4}, {128, 1}, {128, 4}};
-    for (int rep = 0; rep < 2; ++rep)
-      for (auto& c : cfg) {
-        if (c[0] == 128 && (M + 127) / 128 * (N / 128) * 4 > tiles64 * 4) continue;
-        g_node_rows = c[0]; g_node_ksplit = c[1];
-        CK(hipMemset(C, 0, nc * 4));
-        float t = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
-        CK(hipStreamSynchronize(s));
-        CK(hipMemcpy(c1.data(), C, nc * 4, hipMemcpyDeviceToHost));
-        printf("M=%ld N=%d K=%d rows %d ksplit %d: %.2f us %.1f TF fp32-eq  bit-identical to ksplit 1: %s\n", M, N, K,
-               c[0], c[1], t * 1e3, flops / t / 1e9, c0 == c1 ? "yes" : "NO");
-      }
-    g_node_rows = g_node_ksplit = 0;
-    return 0;
-  }
   if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
     CK(node_gemm_init());
     for (int rep = 0; rep < 2; ++rep) {
