@@ -105,6 +105,10 @@ struct EdgeArgs {
   // zero_flags / nzero: an EPI_EDGE launch's block 0 clears them for the next grid.
   unsigned* flags; long flag_row0;
   unsigned* zero_flags; int nzero;
+  // edge layer 1 on unordered pairs (k_edge16_pairs, fc batches, option edge_pairs): A = the pairs' Fourier
+  // features (Mp rows: per crystal the pairs i <= j, row-major), pi / pj = the pair's nodes, pe = its edge
+  // rows {(i, j), (j, i)} (equal for i == j)
+  const int* pi; const int* pj; const int2* pe; long Mp;
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no
@@ -169,6 +173,8 @@ void edge16_seq_jobs(long n, int P, int D, long* out);  // (host) the persistent
 long edge16_layer_blocks(long R, int P);                        // its grid size
 void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its block -> job map
 hipError_t edge16_init();
+// edge layer 1 on unordered pairs: S rows of both directions of every pair from one GEMM row (edge16.hip)
+hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s);
 // (split16.hip) W -> row-scaled split rows (perm 0, or 2 = k_edge16's S column order for W2)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);

@@ -1075,11 +1075,311 @@ __global__ __launch_bounds__(512, 1) void k_edge16_repair(EdgeArgs g, long nvb, 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Edge layer 1 on unordered pairs (option edge_pairs; fc batches). The reference's Fourier features of
+// edge (j, i) are those of edge (i, j) with the sine half negated: frac_diff_ji = (x_i - x_j) % 1 is
+// 1 - frac_diff_ij (or 0 with it), sin(2 pi k (1 - d)) = -sin(2 pi k d), cos(2 pi k (1 - d)) = cos(2 pi k d)
+// (cspnet.py:38-52, 324; exact in real arithmetic; in fp32 the reference's two argument roundings differ
+// by up to 8e-5 on the k = 127 features, which moves the decoder outputs by ~2e-6 of their scale). With
+// V = D_sin f_sin and U = D_cos f_cos over the pair's features, D f_ij = U + V and D f_ji = U - V: one GEMM
+// row of K = 768 per pair (i <= j) instead of two directed rows, half of edge layer 1's matrix work. The K
+// loop runs the 12 sine K-tiles into V, then the 12 cosine K-tiles into U; the epilogue writes both
+// directions' S rows (S_ij = SiLU(U + V + P_i + Q_j), S_ji = SiLU(U - V + P_j + Q_i)) into the directed
+// row layout edge layer 2 reads, exactly as edge16_tile's EPI_EDGE epilogue writes them.
+// Tile: 128 pairs x 256 columns, 8 waves of 32 pairs x 128 columns (two accumulator sets of 64 registers:
+// the budget of edge16_tile's one set of 128); split rows, swizzle, MFMA and C^T layout as edge16_tile.
+namespace {
+constexpr int PBM = 128;                 // pairs per tile
+constexpr int P_NSA = 3, P_NSW = 2;      // ring depths: A (streamed), W (L2-resident)
+constexpr int P_OPA = PBM * ROW_B;       // 16 KB per A stage
+constexpr int P_WRING = P_NSA * P_OPA;   // W stages follow the A stages (32 KB each)
+static_assert(P_WRING + P_NSW * OPND_B <= LDS_B, "LDS");
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;  // rows 32 wm, columns 128 wn of the tile
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const long bid = remap(blockIdx.x, gridDim.x);
+  const int n0 = (int)(bid & 1) * BN;
+  const long row0 = (bid >> 1) * PBM;
+  const long nrows = g.Mp - row0 < PBM ? g.Mp - row0 : PBM;
+  constexpr int nk = FD / BK;        // 24: K-tiles [0, 12) sine features, [12, 24) cosine
+  constexpr int rowB = FD * 4;       // one split row of K = 768
+  // glds: wave w stages A rows 16 w .. 16 w + 15 (2 instructions) and W rows 32 w .. 32 w + 31 (4); lane ->
+  // row base + 8 q + (lane >> 3), LDS chunk lane & 7 holding line chunk (lane & 7) ^ ((row >> 1) & 7)
+  const char* Ablk = reinterpret_cast<const char*>(g.A) + row0 * rowB;
+  const char* Wblk = reinterpret_cast<const char*>(g.W) + (long)n0 * rowB;
+  const int ra0 = wave * 16 + (lane >> 3), rw0 = wave * 32 + (lane >> 3);
+  const unsigned aoff = (unsigned)(ra0 * rowB) + 16u * (unsigned)((lane & 7) ^ ((ra0 >> 1) & 7));
+  const unsigned woff = (unsigned)(rw0 * rowB) + 16u * (unsigned)((lane & 7) ^ ((rw0 >> 1) & 7));
+  const unsigned q8 = (unsigned)(8 * rowB);
+  // (row + 8: its swizzle differs in bit 2, i.e. the source chunk moves by 64 bytes)
+  const unsigned aodd = (((unsigned)(lane & 7) ^ (unsigned)((ra0 >> 1) & 7)) ^ 4u) * 16u - 16u * (unsigned)((lane & 7) ^ ((ra0 >> 1) & 7));
+  const unsigned wodd = (((unsigned)(lane & 7) ^ (unsigned)((rw0 >> 1) & 7)) ^ 4u) * 16u - 16u * (unsigned)((lane & 7) ^ ((rw0 >> 1) & 7));
+  char* dstA = lds + wave * 16 * ROW_B;
+  char* dstW = lds + P_WRING + wave * 32 * ROW_B;
+  auto issueA = [&](int t) __attribute__((always_inline)) {
+    const char* src = Ablk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dstA + (t % P_NSA) * P_OPA;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + aoff + q * q8 + (q & 1 ? aodd : 0u)), (lds_void*)(d + q * 8 * ROW_B),
+                                       16, 0, 0);
+  };
+  auto issueW = [&](int t) __attribute__((always_inline)) {
+    const char* src = Wblk + (long)(t < nk ? t : nk - 1) * ROW_B;
+    char* d = dstW + (t % P_NSW) * OPND_B;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + woff + q * q8 + (q & 1 ? wodd : 0u)), (lds_void*)(d + q * 8 * ROW_B),
+                                       16, 0, 0);
+  };
+
+  f32x4 accV[2][8], accU[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) accV[i][j] = accU[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int swz = (l16 >> 1) & 7;
+  const int ch0 = 16 * (g4 ^ swz), ch1 = 16 * ((4 + g4) ^ swz);
+  const int fa = (wm * 32 + l16) * ROW_B, fw = (wn * 128 + l16) * ROW_B;
+  f16x8 fA[2][2][2];  // [set][plane][row group]
+  f16x8 fW[2][2][2];  // [set][plane][column group of the quarter]
+  auto read_A = [&](int set, int t) __attribute__((always_inline)) {
+    const char* SA = lds + (t % P_NSA) * P_OPA + fa;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      fA[set][0][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch0);
+      fA[set][1][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch1);
+    }
+  };
+  auto read_W = [&](int set, int t, int qq) __attribute__((always_inline)) {
+    const char* SW = lds + P_WRING + (t % P_NSW) * OPND_B + fw + qq * 32 * ROW_B;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      fW[set][0][jj] = *reinterpret_cast<const f16x8*>(SW + jj * 16 * ROW_B + ch0);
+      fW[set][1][jj] = *reinterpret_cast<const f16x8*>(SW + jj * 16 * ROW_B + ch1);
+    }
+  };
+  // one quarter (32 columns of the wave, both row groups, three products: small terms first)
+  auto mfq = [&](f32x4 (&acc)[2][8], int aset, int wset, int qq) __attribute__((always_inline)) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][1][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][1][i], acc[i][2 * qq + jj]);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+  };
+  auto sched_reads = [&](auto NR) __attribute__((always_inline)) {  // NR fragment reads among 12 MFMAs
+    constexpr int nr = decltype(NR)::value;
+#pragma unroll
+    for (int k = 0; k < nr; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 12 - 2 * nr, 0);
+  };
+
+  // prologue (issue order W0 A0 A1 W1 A2): tile 0 has landed when 8 glds remain (A1 2, W1 4, A2 2)
+  issueW(0);
+  issueA(0);
+  issueA(1);
+  issueW(1);
+  issueA(2);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_A(0, 0);
+  read_W(0, 0, 0);
+
+  auto tile = [&](f32x4 (&acc)[2][8], int t, auto CUR) __attribute__((always_inline)) {
+    constexpr int a = decltype(CUR)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
+    __builtin_amdgcn_s_setprio(1);
+    read_W(1, t, 1);
+    mfq(acc, a, 0, 0);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+    read_W(0, t, 2);
+    mfq(acc, a, 1, 1);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_setprio(1);
+    read_W(1, t, 3);
+    mfq(acc, a, 0, 2);
+    sched_reads(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_s_setprio(0);
+    // this wave is done reading tile t; this thread's part of tile t+1 has landed (only A(t+2) may still
+    // be in flight: 2 glds; near the end everything is waited for); after the barrier everyone's has
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (t < nk - 2)
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+    if (t + 2 < nk) issueW(t + 2);
+    if (t + 3 < nk) issueA(t + 3);
+    read_A(a ^ 1, t + 1);  // past the end: reads stale stages (never used)
+    read_W(0, t + 1, 0);
+    mfq(acc, a, 1, 3);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  for (int t = 0; t < nk / 2; t += 2) {  // the sine half of K into V
+    tile(accV, t, std::integral_constant<int, 0>{});
+    tile(accV, t + 1, std::integral_constant<int, 1>{});
+  }
+  for (int t = nk / 2; t < nk; t += 2) {  // the cosine half into U
+    tile(accU, t, std::integral_constant<int, 0>{});
+    tile(accU, t + 1, std::integral_constant<int, 1>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (g.dbg & 16) {  // (profiling: main loop only)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(accU[i][j]), "v"(accV[i][j]));
+    return;
+  }
+
+  // ---- epilogue: undo the W row scales, then per conditioning and direction S = SiLU(U +- V + P + Q)
+  const int cw = n0 + wn * 128 + 4 * g4;  // this lane's first output column (+ 16 j)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(g.wscale + cw + 16 * j);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      accU[i][j] *= sc;
+      accV[i][j] *= sc;
+    }
+  }
+  int ni[2], nj[2];
+  int2 pe[2];
+  bool ok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long lr = wm * 32 + 16 * i + l16;
+    const long p = row0 + (lr < nrows ? lr : nrows - 1);
+    ni[i] = g.pi[p];
+    nj[i] = g.pj[p];
+    pe[i] = g.pe[p];
+    ok[i] = lr < nrows;
+  }
+  _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
+  const bool odd = l16 & 1;
+  const bool nostore = g.dbg & 4;  // (profiling)
+  for (int c = 0; c < g.npairs; ++c) {
+    const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+#pragma unroll
+    for (int dir = 0; dir < 2; ++dir) {
+      static_for<0, 2>([&](auto IC) __attribute__((always_inline)) {
+        constexpr int i = decltype(IC)::value;
+        // forward (i, j): P_i + Q_j, row pe.x; reverse (j, i): P_j + Q_i, row pe.y (none for a self pair)
+        const int rp = dir ? nj[i] : ni[i], rq = dir ? ni[i] : nj[i];
+        const float* prow = Pc + (long)rp * (2 * H) + cw;
+        const float* qrow = Pc + (long)rq * (2 * H) + H + cw;
+        const long orow = (long)c * g.E + (dir ? pe[i].y : pe[i].x);
+        const bool st = ok[i] && !nostore && (dir == 0 || ni[i] != nj[i]);
+        f32x4 v[8];
+        float mx = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(prow + 16 * j);
+          const f32x4 qv = *reinterpret_cast<const f32x4*>(qrow + 16 * j);
+          const f32x4 x = dir ? accU[i][j] - accV[i][j] : accU[i][j] + accV[i][j];
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2e y = silu_e2((f32x2e{x[e], x[e + 1]} + f32x2e{pv[e], pv[e + 1]}) + f32x2e{qv[e], qv[e + 1]});
+            mx = fmaxf(mx, fmaxf(fabsf(y.x), fabsf(y.y)));
+            v[j][e] = y.x;
+            v[j][e + 1] = y.y;
+          }
+        }
+        // the row's 128 columns of this wave sit in the 4 lanes l16 + 16 g
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const int ex2 = exp_of(mx);
+        const float sc = ldexpf(1.0f, -ex2);
+        // whole-line stores as edge16_tile's: lanes l16, l16 ^ 1 swap a piece (DPP) so that one store writes
+        // the even lane's row's whole 128-B line and the next the odd lane's (rows anywhere in S)
+        const long orow_p = ((long)__shfl_xor((int)(orow >> 32), 1, 64) << 32) | (unsigned)__shfl_xor((int)orow, 1, 64);
+        const int st_p = __shfl_xor(st ? 1 : 0, 1, 64);
+        const long orow_e = odd ? orow_p : orow, orow_o = odd ? orow : orow_p;
+        const bool st_e = odd ? st_p != 0 : st, st_o = odd ? st : st_p != 0;
+        const int off = ((n0 + wn * 128) / 32) * 64 + 8 * g4 + (odd ? 32 : 0);
+        _Float16* se = S0 + orow_e * (2 * H) + off;
+        _Float16* so = S0 + orow_o * (2 * H) + off;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {  // 32-column chunks: column groups 2cc, 2cc + 1
+          f16x8 hv, lv;
+#pragma unroll
+          for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float xx = v[2 * cc + a2][r] * sc;
+              const _Float16 hx = (_Float16)xx;
+              hv[4 * a2 + r] = hx;
+              lv[4 * a2 + r] = (_Float16)(xx - (float)hx);
+            }
+          typedef int i32x4 __attribute__((ext_vector_type(4)));
+          const i32x4 snd = __builtin_bit_cast(i32x4, odd ? hv : lv);
+          i32x4 rcv;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) rcv[w] = __builtin_amdgcn_mov_dpp(snd[w], 0xB1, 0xF, 0xF, false);  // lane ^ 1
+          const f16x8 r8 = __builtin_bit_cast(f16x8, rcv);
+          if (st_e) *reinterpret_cast<f16x8*>(se + cc * 64) = odd ? r8 : hv;  // even lane's row: hi (even), lo (odd)
+          if (st_o) *reinterpret_cast<f16x8*>(so + cc * 64) = odd ? lv : r8;  // odd lane's row
+        }
+        if (st && g4 == 0) {
+          signed char* px = reinterpret_cast<signed char*>(g.sexp) + orow * 4 + (n0 + wn * 128) / CHUNK;
+          *px = (signed char)ex2;
+        }
+      });
+    }
+  }
+}
+
+hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s) {
+  if (g.N != H || g.K != FD || !g.A || !g.W || !g.wscale || !g.S || !g.sexp || !g.PQ || !g.pi || !g.pj || !g.pe ||
+      g.Mp < 1 || g.npairs < 1 || g.npairs > 2 || g.nnodes < 1 || g.E < g.Mp)
+    return hipErrorInvalidValue;
+  if (hipError_t e = edge16_init(); e != hipSuccess) return e;
+  const long blocks = (g.Mp + PBM - 1) / PBM * (H / BN);
+  hipLaunchKernelGGL(k_edge16_pairs, dim3((unsigned)blocks), dim3(512), LDS_B, s, g);
+  return hipGetLastError();
+}
+
 static hipError_t edge16_init_once() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
-                      (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>};
+                      (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
+                      (const void*)k_edge16_pairs};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;

@@ -85,6 +85,8 @@ struct chm_model {
   int edge_dyn = 1;      // CHM_EDGE_DYN: one-grid kernel form, 0 static block -> job map (k_edge16_layer), 1 the
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
+  int edge_pairs = 0;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
+                         // half its matrix work; both directions' S from one GEMM row), then edge layer 2
   int ncu = 0;           // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
@@ -105,6 +107,10 @@ struct chm_batch {
   int *natoms, *node_off, *n2g, *ei, *ej;
   long *edge_off, *node_estart;
   int* node_n;  // atom count of each node's crystal
+  // fc: the unordered pairs (i <= j) of every crystal for edge layer 1 on pairs (BatchTables::pi / pj / pe)
+  int *pi = nullptr, *pj = nullptr;
+  int2* pe = nullptr;
+  long Ep = 0;
   int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
   // fc batches: edge layer 2 (k_edge16) on row tiles of exactly 256 edge rows, nodes cut at the tile
@@ -321,6 +327,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (dyn) m->edge_dyn = atoi(dyn);
     const char* pool = getenv("CHM_EDGE_POOL");
     if (pool) m->edge_pool = atoi(pool);
+    const char* pairs = getenv("CHM_EDGE_PAIRS");
+    if (pairs) m->edge_pairs = atoi(pairs);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -465,6 +473,11 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_pool = (int)value;
     return CHM_OK;
   }
+  if (k == "edge_pairs") {  // fc edge layer 1 on unordered pairs (k_edge16_pairs), then edge layer 2 (within fp32
+                            // rounding of the directed edges: DESIGN.md §4 "Edge layer 1 on pairs")
+    m->edge_pairs = value != 0;
+    return CHM_OK;
+  }
   if (k == "edge_lag") {
     if (value < 1 || value > kMaxLag) return fail(CHM_E_ARG, "edge_lag must be in [1, 1000]");
     m->edge_lag = (int)value;
@@ -524,6 +537,10 @@ struct BatchTables {
   std::vector<int> rinfo_n;
   long nrt = 0, r2tot = 0;
   long N = 0, E = 0;  // knn: E = the edge capacity
+  // fc: the unordered pairs i <= j of every crystal, row-major (edge layer 1 on pairs, k_edge16_pairs)
+  std::vector<int> pi, pj;
+  std::vector<int2> pe;
+  long Ep = 0;
   long C = 0;         // knn: candidate scratch entries (sum of n^2 * 27)
   bool knn = false;
 };
@@ -540,6 +557,7 @@ static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t, const Ba
     t.eoff[g] = E;
     N += t.nat[g];
     E += (long)t.nat[g] * t.nat[g];
+    t.Ep += (long)t.nat[g] * (t.nat[g] + 1) / 2;
     if (N > (1L << 30) || E > (1L << 31) - 1) return fail(CHM_E_ARG, "batch too large");
   }
   t.noff[B] = (int)N;
@@ -637,6 +655,18 @@ static void batch_fill(BatchTables& t) {
       t.nn[t.noff[g] + i] = t.nat[g];
     }
   if (t.knn) return;  // (edge tables are built per decoder call)
+  t.pi.resize(t.Ep);
+  t.pj.resize(t.Ep);
+  t.pe.resize(t.Ep);
+  for (int g = 0, p = 0; g < B; ++g) {
+    const int n = t.nat[g], o = t.noff[g];
+    for (int i = 0; i < n; ++i)
+      for (int j = i; j < n; ++j, ++p) {
+        t.pi[p] = o + i;
+        t.pj[p] = o + j;
+        t.pe[p] = make_int2((int)(t.eoff[g] + (long)i * n + j), (int)(t.eoff[g] + (long)j * n + i));
+      }
+  }
   t.ei.resize(E);
   t.ej.resize(E);
   t.estart.resize(N);
@@ -704,6 +734,11 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
   b->node_estart = (long*)carve(N * sizeof(long));
   b->node_n = (int*)carve(N * sizeof(int));
   b->tiles = (int2*)carve(ntiles * sizeof(int2));
+  if (!b->knn && b->Ep > 0) {  // fc: the pair tables of edge layer 1 on pairs
+    b->pi = (int*)carve(b->Ep * sizeof(int));
+    b->pj = (int*)carve(b->Ep * sizeof(int));
+    b->pe = (int2*)carve(b->Ep * sizeof(int2));
+  }
   if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
     b->rtiles = (int4*)carve(b->nrt * sizeof(int4));
     b->rinfo = (int2*)carve((size_t)b->nrt * kRowInfo * sizeof(int2));
@@ -787,6 +822,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->ntiles = t.knn ? (int)(t.N + 1) : (int)t.tiles.size();
   b->nrt = t.knn ? 0 : t.nrt;
   b->r2tot = t.knn ? 0 : t.r2tot;
+  b->Ep = t.knn ? 0 : t.Ep;
   const size_t need = batch_layout(b, m, nullptr, b->ntiles);
   char* base = (char*)d_ws;
   if (!base) {
@@ -838,6 +874,9 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->rtiles, t.rtiles.data(), t.rtiles.size() * sizeof(int4));
     up(b->rinfo, t.rinfo.data(), t.rinfo.size() * sizeof(int2));
     up(b->rinfo_n, t.rinfo_n.data(), t.rinfo_n.size() * sizeof(int));
+    up(b->pi, t.pi.data(), t.pi.size() * sizeof(int));
+    up(b->pj, t.pj.data(), t.pj.size() * sizeof(int));
+    up(b->pe, t.pe.data(), t.pe.size() * sizeof(int2));
     if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
     if (e == hipSuccess && b->lflags) e = hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s);
@@ -923,6 +962,7 @@ extern "C" size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t
   if (!t.knn) {
     b.nrt = (t.E + kTileRows - 1) / kTileRows;
     b.r2tot = row_tiles(t, nullptr);
+    b.Ep = t.Ep;
   }
   return batch_layout(&b, m, nullptr, count_tiles(t));
 }
@@ -1178,7 +1218,11 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
   HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H), ps ? b->Hs : nullptr, ps ? b->He : nullptr));
-  if (b->math == MATH_SPLIT16)
+  // fc edge layer 1 on unordered pairs (option edge_pairs): F holds the pairs' features only
+  const bool pairs = b->math == MATH_SPLIT16 && m->edge_pairs && b->pe && !b->knn && E > 0;
+  if (pairs)
+    HIPCHK(fourier_h(x, b->pi, b->pj, b->Ep, b->F, s, nullptr));  // (the (i, j) edges' features, i <= j)
+  else if (b->math == MATH_SPLIT16)
     HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s, b->knn ? b->fd : nullptr));  // fp16 hi/lo split rows
   else
     HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
@@ -1254,7 +1298,17 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (e2.rtiles && m->edge_layer && b->nrt >= m->edge_layer_min && (!m->edge_trace || m->edge_trace_layer == 3)) {
+      if (pairs) {
+        // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
+        EdgeArgs e1p = e1;
+        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
+        {
+          ProfScope ps(CHM_K_EDGE_FOURIER, s);
+          HIPCHK(edge_gemm16_pairs(e1p, s));
+        }
+        ProfScope ps(CHM_K_EDGE_MESSAGE, s);
+        HIPCHK(edge_gemm16(e2, EPI_SEGMEAN, s));
+      } else if (e2.rtiles && m->edge_layer && b->nrt >= m->edge_layer_min && (!m->edge_trace || m->edge_trace_layer == 3)) {
         // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
         e1.lflags = e2.lflags = b->lflags;
         e1.xbad = e2.xbad = b->xbad + l;
