@@ -1115,7 +1115,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
   const unsigned aoff = (unsigned)(ra0 * rowB) + 16u * (unsigned)((lane & 7) ^ ((ra0 >> 1) & 7));
   const unsigned woff = (unsigned)(rw0 * rowB) + 16u * (unsigned)((lane & 7) ^ ((rw0 >> 1) & 7));
   const unsigned q8 = (unsigned)(8 * rowB);
-  // (row + 8: its swizzle differs in bit 2, i.e. the source chunk moves by 64 bytes)
+  // (row + 8: its swizzle differs in bit 2, i.e. the source chunk moves by 64 bytes; the move is a 32-bit
+  // unsigned difference, so it is added to the offset BEFORE the pointer: offset + move never wraps)
   const unsigned aodd = (((unsigned)(lane & 7) ^ (unsigned)((ra0 >> 1) & 7)) ^ 4u) * 16u - 16u * (unsigned)((lane & 7) ^ ((ra0 >> 1) & 7));
   const unsigned wodd = (((unsigned)(lane & 7) ^ (unsigned)((rw0 >> 1) & 7)) ^ 4u) * 16u - 16u * (unsigned)((lane & 7) ^ ((rw0 >> 1) & 7));
   char* dstA = lds + wave * 16 * ROW_B;
@@ -1125,7 +1126,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
     char* d = dstA + (t % P_NSA) * P_OPA;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + aoff + q * q8 + (q & 1 ? aodd : 0u)), (lds_void*)(d + q * 8 * ROW_B),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (aoff + q * q8 + (q & 1 ? aodd : 0u))), (lds_void*)(d + q * 8 * ROW_B),
                                        16, 0, 0);
   };
   auto issueW = [&](int t) __attribute__((always_inline)) {
@@ -1133,7 +1134,7 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
     char* d = dstW + (t % P_NSW) * OPND_B;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + woff + q * q8 + (q & 1 ? wodd : 0u)), (lds_void*)(d + q * 8 * ROW_B),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (woff + q * q8 + (q & 1 ? wodd : 0u))), (lds_void*)(d + q * 8 * ROW_B),
                                        16, 0, 0);
   };
 
