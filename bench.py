@@ -101,14 +101,31 @@ def edge_layer_bytes(natoms, P=2):
     return f + 2 * s + P * N * 2 * H * 4 + P * N * H * 4 + (H * FD + H * H) * 4
 
 
-def decoder_pair_flops(natoms, P=2, share_fourier=True):
-    """Algorithmic fp32 flops of one decoder call pair as implemented
-    (SURVEY.md §8(d) factorised formula, with the Fourier projection shared
-    by the cond/null pair)."""
+def message_layer_bytes(natoms, P=2):
+    """Algorithmic HBM bytes of one edge-layer-2 launch (k_edge16<EPI_SEGMEAN>: S.W2^T + SiLU + fused
+    scatter_mean, both conditionings): S read once (E x 512 fp16 hi/lo + one packed exponent word per
+    row, per conditioning), agg written, the split weight W2 (512 x 512) read once."""
     E = sum(n * n for n in natoms)
     N = sum(natoms)
+    return P * E * (H * 4 + 4) + P * N * H * 4 + H * H * 4
+
+
+def edge_pairs_on():
+    """Edge layer 1 on unordered pairs (option edge_pairs, the library default; CHM_EDGE_PAIRS=0 turns it off)."""
+    return os.environ.get("CHM_EDGE_PAIRS", "1") != "0"
+
+
+def decoder_pair_flops(natoms, P=2, share_fourier=True, pairs=None):
+    """Algorithmic fp32 flops of one decoder call pair as implemented
+    (SURVEY.md §8(d) factorised formula, with the Fourier projection shared
+    by the cond/null pair; with edge layer 1 on pairs, the Fourier projection
+    once per unordered pair i <= j: sum n(n+1)/2 rows instead of sum n^2)."""
+    E = sum(n * n for n in natoms)
+    Ep = sum(n * (n + 1) // 2 for n in natoms)
+    N = sum(natoms)
     B = len(natoms)
-    edge = E * L * ((1 if share_fourier else P) * 2 * FD * H + P * 2 * H * H)
+    pairs = edge_pairs_on() if pairs is None else pairs
+    edge = L * ((1 if share_fourier else P) * 2 * FD * H * (Ep if pairs else E) + E * P * 2 * H * H)
     node = P * N * L * (4 * H * H + 2 * (2 * H * H + H * H) + 2 * H * H)
     heads = P * N * 2 * H * 107 + P * B * 2 * 640 * 2 * H
     return edge + node + heads
@@ -535,7 +552,9 @@ def main():
     seg_bytes = 2.0 * (E * H * 4 + N * H * 4)
     step_flops = 2 * decoder_pair_flops(natoms)
     math = model.decoder.get_math()
-    fou_flops = 2.0 * E * 768 * H  # edge layer 1: D.f once for both conditionings
+    Ep = sum(n * (n + 1) // 2 for n in natoms)
+    fou_flops = 2.0 * (Ep if edge_pairs_on() else E) * 768 * H  # edge layer 1: D.f once for both conditionings
+    # (on pairs: once per unordered pair, k_edge16_pairs)
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
     msg_kernel = "k_edge16_layer" if nlay else "k_edge16<2"
     traffic, traffic_src = None, "not collected for the ragged workload" if args.ragged else "not collected"
@@ -628,7 +647,7 @@ def main():
                      "mfma_busy": (traffic_src.get("mfma_busy") if isinstance(traffic_src, dict) else None),
                      "mfma_busy_note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), in-run PMC "
                                        "pass over the same probe as traffic",
-                     "traffic_algorithmic": (edge_layer_bytes(natoms) if nlay else None),
+                     "traffic_algorithmic": (edge_layer_bytes(natoms) if nlay else message_layer_bytes(natoms)),
                      "peak_note": {"bf16x3": "fp32-equivalent flops; bf16 dense MFMA 2.5 PF / 6 products",
                                    "split16": "fp32-equivalent flops (3 fp16 MFMA products each); fp16 dense MFMA "
                                            "2.5 PF / 3 products",
@@ -647,7 +666,10 @@ def main():
                         "achieved": msg_tflops, "peak": peak, "unit": "TFLOP/s",
                         "frac": (msg_tflops / peak) if msg_tflops else None, "flops_per_launch": msg_flops,
                         "avg_ms": ms_msg / nmsg if nmsg else None},
-        "edge_layer1": {"kernel": "edge layer 1 (D.f + P_i + Q_j + SiLU, S written split), both conditionings",
+        "edge_layer1": {"kernel": ("edge layer 1 on unordered pairs (k_edge16_pairs: D.f once per pair i <= j, both "
+                                   "directions' S = SiLU(U +- V + P + Q) written split), both conditionings"
+                                   if edge_pairs_on() else
+                                   "edge layer 1 (D.f + P_i + Q_j + SiLU, S written split), both conditionings"),
                         "achieved": fou_tflops, "peak": peak, "unit": "TFLOP/s",
                         "frac": (fou_tflops / peak) if fou_tflops else None, "flops_per_launch": fou_flops,
                         "avg_ms": ms_fou / nfou if nfou else None},

@@ -85,7 +85,7 @@ struct chm_model {
   int edge_dyn = 1;      // CHM_EDGE_DYN: one-grid kernel form, 0 static block -> job map (k_edge16_layer), 1 the
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
-  int edge_pairs = 0;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
+  int edge_pairs = 1;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
   int ncu = 0;           // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)

@@ -321,6 +321,7 @@ def test_edge_tail_split_is_bit_identical(cn, nat):
     nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
           torch.randn(N, 3, generator=g))
     model = _model(1000)  # its own instance: the option stays out of the shared fixtures
+    model.decoder.set_option("edge_pairs", 0)  # (the directed edge-layer-1 schedules under test)
     outs = []
     for split in (1, 0):
         model.decoder.set_option("edge_split", split)
@@ -347,6 +348,7 @@ def test_edge_tail_timeout_is_flagged_and_repaired(cn):
     nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
           torch.randn(N, 3, generator=g))
     model = _model(1000)
+    model.decoder.set_option("edge_pairs", 0)  # (the directed edge-layer-1 schedules under test)
     model.decoder.set_option("edge_layer", 0)  # (the one-grid kernel would take this shape)
     outs, events = [], []
     for split, timeout, norepair in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)):
@@ -392,6 +394,7 @@ def test_edge_row_tiles_are_bit_identical(cn, nat):
     nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
           torch.randn(N, 3, generator=g))
     model = _model(1000)
+    model.decoder.set_option("edge_pairs", 0)  # (the directed edge-layer-1 schedules under test)
     outs = []
     _lib.prof_events(reset=True)
     for rows, nowait, layer, lag, repair, dyn in ((0, 0, 0, 10, 0, 2), (1, 0, 0, 10, 0, 2), (1, 1, 0, 10, 0, 2),
@@ -436,6 +439,7 @@ def test_persistent_edge_kernel_with_a_missing_xcd_is_repaired(cn, nat):
     nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
           torch.randn(N, 3, generator=g))
     model = _model(1000)
+    model.decoder.set_option("edge_pairs", 0)  # (the directed edge-layer-1 schedules under test)
     outs, events = [], []
     for dyn, skip in ((0, -1), (2, -1), (2, 5)):
         model.decoder.set_option("edge_layer_dyn", dyn)
@@ -497,6 +501,7 @@ def test_one_grid_edge_layers_single_conditioning(cn):
     ragged batch, decoder outputs bit-identical to the two-launch schedule, also with the repair
     launches forced."""
     model = _model(1000)
+    model.decoder.set_option("edge_pairs", 0)  # (the directed edge-layer-1 schedules under test)
     for nat in ([40] * 64, torch.randint(1, 81, (160,), generator=torch.Generator().manual_seed(5)).tolist()):
         B, N = len(nat), sum(nat)
         g = torch.Generator().manual_seed(21)
@@ -848,7 +853,33 @@ def test_edge_pairs_match_directed_edges(model1000, cn, nat):
     for on in (0, 1):
         dec.set_option("edge_pairs", on)
         outs.append([o.cpu() for o in dec.forward_cfg(a, x, lat, nat, te, c, n, need_nodes=True)])
-    dec.set_option("edge_pairs", 0)
+    dec.set_option("edge_pairs", 1)  # (the default)
     errs = [close(p, d, rtol=2e-5, what=f"edge_pairs {name}")
             for name, d, p in zip(("types", "lattice", "coords", "nodes"), *outs)]
     assert max(errs) > 0  # (the option really changed the arithmetic path)
+
+
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9])
+def test_edge_pairs_layer2_schedules_are_bit_identical(cn, nat):
+    """With edge layer 1 on pairs (the default), edge layer 2's schedules stay bit-identical to one another:
+    node-aligned segment tiles, row tiles, and row tiles with the msgbuf path forced ('edge_rows_nowait'),
+    and the step is reproducible."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(16)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    model.decoder.set_option("edge_pairs", 1)
+    outs = []
+    for rows, nowait in ((0, 0), (1, 0), (1, 1), (1, 0)):
+        model.decoder.set_option("edge_rows", rows)
+        model.decoder.set_option("edge_rows_nowait", nowait)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+    del model
+    torch.cuda.empty_cache()
+    for k in (1, 2, 3):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: edge-pairs layer-2 schedule {k} differs"
