@@ -1304,8 +1304,10 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
         const int rp = dir ? nj[i] : ni[i], rq = dir ? ni[i] : nj[i];
         const float* prow = Pc + (long)rp * (2 * H) + cw;
         const float* qrow = Pc + (long)rq * (2 * H) + H + cw;
-        const long orow = (long)c * g.E + (dir ? pe[i].y : pe[i].x);
-        const bool st = ok[i] && !nostore && (dir == 0 || ni[i] != nj[i]);
+        // (dbg 131072 / 262144, profiling: no reverse-direction stores / the reverse rows stored at the forward
+        // rows' places: what the scattered reverse rows cost; wrong results)
+        const long orow = (long)c * g.E + (dir && !(g.dbg & 262144) ? pe[i].y : pe[i].x);
+        const bool st = ok[i] && !nostore && (dir == 0 || (ni[i] != nj[i] && !(g.dbg & 131072)));
         f32x4 v[8];
         float mx = 0.f;
 #pragma unroll
