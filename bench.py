@@ -89,14 +89,15 @@ def parse():
     return p.parse_args()
 
 
-def edge_layer_bytes(natoms, P=2):
+def edge_layer_bytes(natoms, P=2, pairs=None):
     """Algorithmic HBM bytes of one k_edge16_layer launch (both edge layers of a CSP layer, split16):
     F read once (E x 768 fp16 hi/lo), S written and read once per conditioning (E x 512 fp16 hi/lo +
     one packed exponent word per row), the P / Q node halves read, agg written, the split weights
     D (512 x 768) and W2 (512 x 512) read once."""
     E = sum(n * n for n in natoms)
     N = sum(natoms)
-    f = E * FD * 4
+    pairs = edge_pairs_on() if pairs is None else pairs
+    f = (sum(n * (n + 1) // 2 for n in natoms) if pairs else E) * FD * 4  # (on pairs: one feature row per pair)
     s = P * E * (H * 4 + 4)
     return f + 2 * s + P * N * 2 * H * 4 + P * N * H * 4 + (H * FD + H * H) * 4
 
@@ -556,7 +557,7 @@ def main():
     fou_flops = 2.0 * (Ep if edge_pairs_on() else E) * 768 * H  # edge layer 1: D.f once for both conditionings
     # (on pairs: once per unordered pair, k_edge16_pairs)
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
-    msg_kernel = "k_edge16_layer" if nlay else "k_edge16<2"
+    msg_kernel = ("k_edge16_pairs_layer" if edge_pairs_on() else "k_edge16_layer") if nlay else "k_edge16<2"
     traffic, traffic_src = None, "not collected for the ragged workload" if args.ragged else "not collected"
     if math == "split16" and not args.ragged:
         if rank == 0 and world == 1 and not args.no_traffic:
@@ -631,10 +632,15 @@ def main():
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
-                     "kernel": {"split16": ("both edge layers of a CSP layer in one grid (k_edge16_layer: D.f + P_i + "
-                                            "Q_j + SiLU -> S, S.W2^T + SiLU + fused scatter_mean; 16x16x32 MFMA), "
-                                            "both conditionings, incl. its two repair launches (no-ops unless a "
-                                            "check fails)") if nlay else
+                     "kernel": {"split16": (("both edge layers of a CSP layer in one persistent grid, layer 1 on "
+                                             "unordered pairs (k_edge16_pairs_layer: D.f once per pair i <= j, both "
+                                             "directions' S = SiLU(U +- V + P + Q); S.W2^T + SiLU + fused "
+                                             "scatter_mean; 16x16x32 MFMA), both conditionings, incl. its three repair "
+                                             "launches (no-ops unless a check fails)") if edge_pairs_on() else
+                                            ("both edge layers of a CSP layer in one grid (k_edge16_layer: D.f + P_i + "
+                                             "Q_j + SiLU -> S, S.W2^T + SiLU + fused scatter_mean; 16x16x32 MFMA), "
+                                             "both conditionings, incl. its two repair launches (no-ops unless a "
+                                             "check fails)")) if nlay else
                                            (f"edge message GEMM + fused scatter_mean ({msg_kernel}, EPI_SEGMEAN, "
                                             "16x16x32 MFMA), both conditionings"),
                                 "bf16x3": "edge message GEMM + fused scatter_mean (k_gemm3_big<EPI_SEGMEAN>), "

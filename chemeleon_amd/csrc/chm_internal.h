@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace chm {
 
 constexpr int H = 512;       // hidden_dim (the build implements the shipped config)
@@ -175,6 +177,38 @@ void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its b
 hipError_t edge16_init();
 // edge layer 1 on unordered pairs: S rows of both directions of every pair from one GEMM row (edge16.hip)
 hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s);
+// Both edge layers of a CSP layer in one persistent grid with edge layer 1 on pairs (k_edge16_pairs_layer):
+// XCD x runs the row tiles [R x / 8, R (x + 1) / 8) of edge layer 2 and every pair tile they read (the tiles of
+// two neighbouring XCDs' ranges may overlap: both compute them, identically), each from a host-built job list
+// (pair tiles in order, a row tile's 2 P layer-2 jobs placed `lag` pair tiles behind the last pair tile it reads).
+// A layer-2 job waits (bounded) until its XCD has finished every pair tile of its range, so S goes through the
+// XCD's L2. Per batch and layer: cnt [8] job counters, pflag [8][npx] finished column tiles per pair tile, done
+// (finished layer-2 jobs | exited blocks << 32), all zeroed per decoder call.
+struct PairSched {
+  const int2* jobs;    // [8][jstride] {kind, tile index}: kind 1 = pair (pair tile * 2 + column tile), 2 = layer 2
+                       // ((row tile * P + conditioning) * 2 + column tile)
+  const int* njobs;    // [8]
+  int jstride;
+  const int2* rng;     // [R] the pair tiles [lo, hi] row tile t reads
+  const int* pa;       // [8] XCD x's first pair tile
+  int npx;             // pflag entries per XCD
+  unsigned* cnt;       // [8]
+  unsigned* pflag;     // [8][npx]
+  unsigned long long* done;
+  long R;
+  int skip_x;          // (tests) the blocks on this XCD exit at once: the launch's self-check must catch it
+};
+hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
+                                   int repair_grid, hipStream_t s);
+// (host) XCD job lists of k_edge16_pairs_layer for an fc batch: row tiles' pair-tile ranges, per XCD its first
+// pair tile and job list (lag in pair tiles)
+struct PairPlan {
+  std::vector<int2> rng;
+  std::vector<int> pa, pb, njobs;
+  std::vector<int2> jobs;  // [8][jstride]
+  int jstride = 0, npx = 0;
+};
+void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int lag, PairPlan& out);
 // (split16.hip) W -> row-scaled split rows (perm 0, or 2 = k_edge16's S column order for W2)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);

@@ -21,6 +21,7 @@
 // index is split with the same permutation (split_rows_h perm 2).
 #include "chm_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace chm {
@@ -1096,12 +1097,12 @@ constexpr int P_WRING = P_NSA * P_OPA;   // W stages follow the A stages (32 KB 
 static_assert(P_WRING + P_NSW * OPND_B <= LDS_B, "LDS");
 }  // namespace
 
-__global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
+// one pair tile: bid = pair tile * 2 + column tile (tid_in: the persistent kernel's opaque copy of threadIdx.x)
+__device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_in) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = tid_in, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // rows 32 wm, columns 128 wn of the tile
   const int l16 = lane & 15, g4 = lane >> 4;
-  const long bid = remap(blockIdx.x, gridDim.x);
   const int n0 = (int)(bid & 1) * BN;
   const long row0 = (bid >> 1) * PBM;
   const long nrows = g.Mp - row0 < PBM ? g.Mp - row0 : PBM;
@@ -1296,8 +1297,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
   const bool nostore = g.dbg & 4;  // (profiling)
   for (int c = 0; c < g.npairs; ++c) {
     const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
-#pragma unroll
-    for (int dir = 0; dir < 2; ++dir) {
+    static_for<0, 2>([&](auto DIR) __attribute__((always_inline)) {
+      constexpr int dir = decltype(DIR)::value;
       static_for<0, 2>([&](auto IC) __attribute__((always_inline)) {
         constexpr int i = decltype(IC)::value;
         // forward (i, j): P_i + Q_j, row pe.x; reverse (j, i): P_j + Q_i, row pe.y (none for a self pair)
@@ -1363,8 +1364,14 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
           *px = (signed char)ex2;
         }
       });
-    }
+    });
   }
+}
+
+__global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
+  // (repair launches, g.xbad set: run only when the one-grid launch before raised its repair request)
+  if (g.xbad && __hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  pair_tile(g, remap(blockIdx.x, gridDim.x), threadIdx.x);
 }
 
 hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s) {
@@ -1377,12 +1384,178 @@ hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Both edge layers of a CSP layer in one persistent grid, edge layer 1 on pairs (chm_internal.h PairSched).
+// The directed one-grid kernel (k_edge16_layer_dyn) pairs layer-1 row tile t with layer-2 row tile t; on pairs,
+// layer-2 row tile t reads the S rows of every pair tile of its crystals up to its last node's pair row, a
+// contiguous range [lo(t), hi(t)] (pair_plan). Each XCD runs a contiguous range of row tiles and all the pair
+// tiles they read, so every S row a layer-2 tile reads was written through the same XCD's L2. Ranges of
+// neighbouring XCDs may share a pair tile: both compute it and write identical bytes.
+void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int lag, PairPlan& out) {
+  const int B = (int)nat.size();
+  std::vector<long> eoff(B + 1, 0), poff(B + 1, 0);
+  for (int g = 0; g < B; ++g) {
+    eoff[g + 1] = eoff[g] + (long)nat[g] * nat[g];
+    poff[g + 1] = poff[g] + (long)nat[g] * (nat[g] + 1) / 2;
+  }
+  auto crystal_of = [&](long row) {  // the crystal holding directed edge row `row`
+    return (int)(std::upper_bound(eoff.begin(), eoff.end(), row) - eoff.begin()) - 1;
+  };
+  out.rng.assign(R, make_int2(0, 0));
+  for (long t = 0; t < R; ++t) {
+    const long r0 = t * BM, r1 = (t * BM + BM < E ? t * BM + BM : E) - 1;
+    const int g0 = crystal_of(r0), g1 = crystal_of(r1);
+    const long n1 = nat[g1], i1 = (r1 - eoff[g1]) / n1;
+    // first pair of the first crystal (the first node's reverse rows read pairs from its crystal's start);
+    // last pair of the last node's pair row (its forward rows)
+    const long lo = poff[g0], hi = poff[g1] + i1 * n1 - i1 * (i1 - 1) / 2 + (n1 - 1 - i1);
+    out.rng[t] = make_int2((int)(lo / PBM), (int)(hi / PBM));
+  }
+  const long NP = (Ep + PBM - 1) / PBM;
+  out.pa.assign(8, 0);
+  out.pb.assign(8, 0);
+  out.njobs.assign(8, 0);
+  std::vector<std::vector<int2>> jl(8);
+  for (int x = 0; x < 8; ++x) {
+    const long ra = R * x / 8, rb = R * (x + 1) / 8;
+    if (ra >= rb) continue;
+    const int pa = out.rng[ra].x, pb = out.rng[rb - 1].y + 1;
+    out.pa[x] = pa;
+    out.pb[x] = pb < NP ? pb : (int)NP;
+    long t = ra;
+    auto emit_row = [&](long tt) {
+      for (int c = 0; c < P; ++c)
+        for (int col = 0; col < 2; ++col) jl[x].push_back(make_int2(2, (int)((tt * P + c) * 2 + col)));
+    };
+    for (int p = pa; p < out.pb[x]; ++p) {
+      jl[x].push_back(make_int2(1, p * 2));
+      jl[x].push_back(make_int2(1, p * 2 + 1));
+      for (; t < rb && out.rng[t].y + lag <= p; ++t) emit_row(t);
+    }
+    for (; t < rb; ++t) emit_row(t);
+    out.njobs[x] = (int)jl[x].size();
+  }
+  out.jstride = 0;
+  out.npx = 1;
+  for (int x = 0; x < 8; ++x) {
+    out.jstride = std::max(out.jstride, out.njobs[x]);
+    out.npx = std::max(out.npx, out.pb[x] - out.pa[x]);
+  }
+  out.jobs.assign((size_t)8 * out.jstride, make_int2(0, 0));
+  for (int x = 0; x < 8; ++x) std::copy(jl[x].begin(), jl[x].end(), out.jobs.begin() + (size_t)x * out.jstride);
+}
+
+__global__ __launch_bounds__(512, 1) void k_edge16_pairs_layer(EdgeArgs g1, EdgeArgs g2, PairSched ps) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const unsigned x = xcc_id();
+  const int P = g2.npairs;
+  int* bc = reinterpret_cast<int*>(lds);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int code = 0, idx = 0;
+      if ((int)x != ps.skip_x) {
+        const unsigned k = __hip_atomic_fetch_add(ps.cnt + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)k < ps.njobs[x]) {
+          const int2 j = ps.jobs[(long)x * ps.jstride + k];
+          code = j.x;
+          idx = j.y;
+          if (code == 2) {  // wait (bounded) until this XCD has finished both column tiles of every pair tile read
+            const int2 r = ps.rng[idx / (2 * P)];
+            bool late = false;
+            for (int p = r.x; p <= r.y && !late; ++p) {
+              const unsigned* f = ps.pflag + (long)x * ps.npx + (p - ps.pa[x]);
+              unsigned spins = 0;
+              while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 2u && ++spins < (1u << 21))
+                __builtin_amdgcn_s_sleep(4);
+              late = spins >= (1u << 21);
+            }
+            if (late) {  // (never in a healthy run: the layer is recomputed by the repair launches)
+              __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              count_event(EV_LAYER_TIMEOUT);
+            }
+          }
+        }
+      }
+      if (code == 0) {  // exit; the last block out checks that every layer-2 job ran (the 8-XCD assumption)
+        const unsigned long long old = __hip_atomic_fetch_add(ps.done, 1ull << 32, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        if ((old >> 32) + 1ull == (unsigned long long)gridDim.x) {
+          if ((old & 0xffffffffull) != (unsigned long long)ps.R * P * 2) {
+            __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            count_event(EV_LAYER_INCOMPLETE);
+          } else if (g2.dbg & 512) {  // (tests, option edge_layer_repair: the repair launches always run)
+            __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      bc[0] = code;
+      bc[1] = idx;
+    }
+    __syncthreads();
+    const int code = bc[0], idx = bc[1];
+    __syncthreads();
+    if (code == 0) break;
+    // (laundered kernarg pointers, as k_edge16_layer_dyn: the tiles read their arguments from memory)
+    typedef const __attribute__((address_space(4))) char* kptr;
+    kptr kp = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    constexpr long off2 = (sizeof(EdgeArgs) + alignof(EdgeArgs) - 1) / alignof(EdgeArgs) * alignof(EdgeArgs);
+    const EdgeArgs* a1 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)kp;
+    const EdgeArgs* a2 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)(kp + off2);
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    if (code == 1) {
+      pair_tile(*a1, idx, tid);
+      // every store of this tile has reached the XCD's L2; count the column tile
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(ps.pflag + (long)x * ps.npx + (idx / 2 - ps.pa[x]), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      edge16_tile<EPI_SEGMEAN, true>(*a2, 0, 0, idx, tid);
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
+                                   int repair_grid, hipStream_t s) {
+  if (g1.N != H || g1.K != FD || !g1.A || !g1.W || !g1.wscale || !g1.S || !g1.sexp || !g1.PQ || !g1.pi || !g1.pj ||
+      !g1.pe || g1.Mp < 1 || g1.npairs != g2.npairs || g1.E < g1.Mp || !g1.xbad || g1.xbad != g2.xbad)
+    return hipErrorInvalidValue;
+  if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.rtiles || !g2.sbuf || !g2.msgbuf || !g2.rcnt || !g2.agg ||
+      !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags ||
+      (long)g2.ntiles != ps.R || (long)g2.ntiles * BM < g2.E)
+    return hipErrorInvalidValue;
+  if (!ps.jobs || !ps.njobs || !ps.rng || !ps.pa || !ps.cnt || !ps.pflag || !ps.done || grid < 1)
+    return hipErrorInvalidValue;
+  if (hipError_t e = edge16_init(); e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_edge16_pairs_layer, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, ps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || (g1.dbg & 16384)) return e;  // (dbg 16384: profiling / tests, no repair launches)
+  // the repair launches (exit at once unless a wait timed out or layer-2 jobs are missing): clear layer 2's
+  // agg row maxima and row-tile counters, recompute every pair tile, then every layer-2 tile (two launches)
+  const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
+  EdgeArgs r1 = g1, r2 = g2;
+  hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, 0L, g2.agg_max,
+                     g2.agg_max ? (long)g2.npairs * g2.nnodes : 0L, (unsigned*)nullptr, 0L, -1, g2.rcnt,
+                     (long)g2.npairs * g2.ntiles * 8);
+  const long nb1 = (g1.Mp + PBM - 1) / PBM * (H / BN);
+  hipLaunchKernelGGL(k_edge16_pairs, dim3((unsigned)nb1), dim3(512), LDS_B, s, r1);
+  const long nb2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
+  hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nb2, (unsigned*)nullptr,
+                     0L, (unsigned*)nullptr, 0L, (int)EV_LAYER_REPAIR);
+  return hipGetLastError();
+}
+
 static hipError_t edge16_init_once() {
   const void* ks[] = {(const void*)k_edge16<EPI_STD, false>, (const void*)k_edge16<EPI_EDGE, false>,
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
-                      (const void*)k_edge16_pairs};
+                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_layer};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;

@@ -111,6 +111,12 @@ struct chm_batch {
   int *pi = nullptr, *pj = nullptr;
   int2* pe = nullptr;
   long Ep = 0;
+  // fc, split16: the job lists of both edge layers in one persistent grid on pairs (k_edge16_pairs_layer),
+  // built for P = max_pairs and the model's edge_lag at creation; per layer 16 + 8 npx scheduling words
+  PairPlan pplan;
+  int2 *pjobs = nullptr, *prng = nullptr;
+  int *pnjobs = nullptr, *ppa = nullptr;
+  unsigned* psched = nullptr;
   int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
   // fc batches: edge layer 2 (k_edge16) on row tiles of exactly 256 edge rows, nodes cut at the tile
@@ -739,6 +745,13 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->pj = (int*)carve(b->Ep * sizeof(int));
     b->pe = (int2*)carve(b->Ep * sizeof(int2));
   }
+  if (!b->pplan.jobs.empty()) {  // (and the one-grid pair schedule: job lists, ranges, per-layer words)
+    b->pjobs = (int2*)carve(b->pplan.jobs.size() * sizeof(int2));
+    b->prng = (int2*)carve(b->pplan.rng.size() * sizeof(int2));
+    b->pnjobs = (int*)carve(8 * sizeof(int));
+    b->ppa = (int*)carve(8 * sizeof(int));
+    b->psched = (unsigned*)carve((size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned));
+  }
   if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
     b->rtiles = (int4*)carve(b->nrt * sizeof(int4));
     b->rinfo = (int2*)carve((size_t)b->nrt * kRowInfo * sizeof(int2));
@@ -823,6 +836,8 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->nrt = t.knn ? 0 : t.nrt;
   b->r2tot = t.knn ? 0 : t.r2tot;
   b->Ep = t.knn ? 0 : t.Ep;
+  if (!t.knn && b->math == MATH_SPLIT16 && t.E > 0)
+    pair_plan(t.nat, t.E, t.Ep, t.nrt, b->P, m->edge_lag, b->pplan);
   const size_t need = batch_layout(b, m, nullptr, b->ntiles);
   char* base = (char*)d_ws;
   if (!base) {
@@ -877,6 +892,12 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->pi, t.pi.data(), t.pi.size() * sizeof(int));
     up(b->pj, t.pj.data(), t.pj.size() * sizeof(int));
     up(b->pe, t.pe.data(), t.pe.size() * sizeof(int2));
+    if (b->pjobs) {
+      up(b->pjobs, b->pplan.jobs.data(), b->pplan.jobs.size() * sizeof(int2));
+      up(b->prng, b->pplan.rng.data(), b->pplan.rng.size() * sizeof(int2));
+      up(b->pnjobs, b->pplan.njobs.data(), 8 * sizeof(int));
+      up(b->ppa, b->pplan.pa.data(), 8 * sizeof(int));
+    }
     if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
     if (e == hipSuccess && b->lflags) e = hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s);
@@ -963,6 +984,7 @@ extern "C" size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t
     b.nrt = (t.E + kTileRows - 1) / kTileRows;
     b.r2tot = row_tiles(t, nullptr);
     b.Ep = t.Ep;
+    if (b.math == MATH_SPLIT16 && t.E > 0) pair_plan(t.nat, t.E, t.Ep, b.nrt, b.P, m->edge_lag, b.pplan);
   }
   return batch_layout(&b, m, nullptr, count_tiles(t));
 }
@@ -1243,6 +1265,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     if (m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
+    if (b->psched && m->edge_pairs && m->edge_layer)
+      HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
@@ -1298,7 +1322,20 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (pairs) {
+      if (pairs && e2.rtiles && m->edge_layer && b->psched && P == b->P && b->nrt >= m->edge_layer_min &&
+          m->ncu > 0 && m->xcd_mask == 0xffu) {
+        // both edge layers in one persistent grid, layer 1 on pairs (k_edge16_pairs_layer)
+        EdgeArgs e1p = e1;
+        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
+        e1p.xbad = e2.xbad = b->xbad + l;
+        PairSched ps;
+        unsigned* w = b->psched + (size_t)l * (16 + 8 * b->pplan.npx);
+        ps.jobs = b->pjobs; ps.njobs = b->pnjobs; ps.jstride = b->pplan.jstride; ps.rng = b->prng; ps.pa = b->ppa;
+        ps.npx = b->pplan.npx; ps.cnt = w; ps.done = reinterpret_cast<unsigned long long*>(w + 8);
+        ps.pflag = w + 16; ps.R = b->nrt; ps.skip_x = m->edge_skip_xcd;
+        ProfScope ps_(CHM_K_EDGE_LAYER, s);
+        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->ncu, m->repair_grid, s));
+      } else if (pairs) {
         // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
         EdgeArgs e1p = e1;
         e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
