@@ -116,6 +116,9 @@ SIGNATURES = {
                                       c_i64, c_void_p, c_void_p]),
     "chm_debug_layer_jobs": (c_i64, [c_i64, c_int, c_int, ctypes.POINTER(c_i64), c_i64]),
     "chm_debug_layer_seq": (c_int, [c_i64, c_int, c_int, ctypes.POINTER(c_i64)]),
+    "chm_debug_pair_plan": (c_i64, [ctypes.POINTER(ctypes.c_int32), c_int, c_int, c_int, ctypes.POINTER(ctypes.c_int32),
+                                    c_i64, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), c_i64]),
     "chm_debug_row_nodes": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64,
                                     ctypes.POINTER(ctypes.c_int32), c_i64]),
     "chm_debug_row_tiles": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64,

@@ -87,7 +87,10 @@ struct chm_model {
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int edge_pairs = 1;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
-  int ncu = 0;           // compute units of the device the model lives on
+  int edge_pairs_layer = 0;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
+                             // persistent grid (k_edge16_pairs_layer). Experimental, off: its first GPU run
+                             // faulted (DESIGN.md §4 "Edge layer 1 on pairs"); the two-launch form is validated
+  int ncu = 0;          // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
   int edge_skip_xcd = -1;  // (tests) option edge_dyn_skip_xcd: the persistent kernel's blocks on that XCD exit
@@ -335,6 +338,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (pool) m->edge_pool = atoi(pool);
     const char* pairs = getenv("CHM_EDGE_PAIRS");
     if (pairs) m->edge_pairs = atoi(pairs);
+    const char* player = getenv("CHM_EDGE_PAIRS_LAYER");
+    if (player) m->edge_pairs_layer = atoi(player);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -482,6 +487,10 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
   if (k == "edge_pairs") {  // fc edge layer 1 on unordered pairs (k_edge16_pairs), then edge layer 2 (within fp32
                             // rounding of the directed edges: DESIGN.md §4 "Edge layer 1 on pairs")
     m->edge_pairs = value != 0;
+    return CHM_OK;
+  }
+  if (k == "edge_pairs_layer") {  // (experimental, off) both edge layers on pairs in one grid (k_edge16_pairs_layer)
+    m->edge_pairs_layer = value != 0;
     return CHM_OK;
   }
   if (k == "edge_lag") {
@@ -1018,6 +1027,27 @@ extern "C" void chm_batch_destroy(chm_batch* b) {
 extern "C" size_t chm_batch_device_bytes(const chm_batch* b) { return b ? b->bytes : 0; }
 extern "C" int64_t chm_batch_num_nodes(const chm_batch* b) { return b ? b->N : -1; }
 extern "C" int64_t chm_batch_num_edges(const chm_batch* b) { return b ? b->E : -1; }
+// (host only, tests) the one-grid pair schedule of an fc batch: see include/chemeleon_hip.h
+extern "C" int64_t chm_debug_pair_plan(const int32_t* h_natoms, int B, int P, int lag, int32_t* rng, int64_t cap_rng,
+                                       int32_t* pa, int32_t* pb, int32_t* njobs, int32_t* jobs, int64_t cap_jobs) {
+  if (!h_natoms || B < 1 || P < 1 || P > 2 || lag < 1) return fail(CHM_E_ARG, "bad arguments");
+  BatchTables t;
+  if (int rc = batch_tables(h_natoms, B, t)) return rc;
+  const long R = (t.E + kTileRows - 1) / kTileRows;
+  PairPlan pl;
+  pair_plan(t.nat, t.E, t.Ep, R, P, lag, pl);
+  if (rng && cap_rng >= 2 * R)
+    for (long k = 0; k < R; ++k) { rng[2 * k] = pl.rng[k].x; rng[2 * k + 1] = pl.rng[k].y; }
+  for (int x = 0; x < 8; ++x) {
+    if (pa) pa[x] = pl.pa[x];
+    if (pb) pb[x] = pl.pb[x];
+    if (njobs) njobs[x] = pl.njobs[x];
+  }
+  if (jobs && cap_jobs >= 2L * 8 * pl.jstride)
+    for (size_t k = 0; k < pl.jobs.size(); ++k) { jobs[2 * k] = pl.jobs[k].x; jobs[2 * k + 1] = pl.jobs[k].y; }
+  return pl.jstride;
+}
+
 extern "C" int chm_batch_device(const chm_batch* b) { return b ? b->m->device : fail(CHM_E_ARG, "batch is NULL"); }
 extern "C" int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn) {
   if (!b) return fail(CHM_E_ARG, "batch is NULL");
@@ -1265,7 +1295,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     if (m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
-    if (b->psched && m->edge_pairs && m->edge_layer)
+    if (b->psched && m->edge_pairs && m->edge_pairs_layer && m->edge_layer)
       HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
@@ -1322,7 +1352,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      if (pairs && e2.rtiles && m->edge_layer && b->psched && P == b->P && b->nrt >= m->edge_layer_min &&
+      if (pairs && m->edge_pairs_layer && e2.rtiles && m->edge_layer && b->psched && P == b->P &&
+          b->nrt >= m->edge_layer_min &&
           m->ncu > 0 && m->xcd_mask == 0xffu) {
         // both edge layers in one persistent grid, layer 1 on pairs (k_edge16_pairs_layer)
         EdgeArgs e1p = e1;
