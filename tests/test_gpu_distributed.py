@@ -55,7 +55,7 @@ def _worker(rank, world, port, q):
         if rank != 0:  # only rank 0 holds the text-encoder output; the broadcast must deliver it
             cond, null = torch.zeros_like(cond), torch.zeros_like(null)
         a, x, lat, nat = sample_distributed(m, NAT, cond.cuda(), null.cuda(), seed=3, noise="philox")
-        q.put((rank, a.cpu(), x.cpu(), lat.cpu(), nat))
+        q.put((rank, a.cpu().numpy(), x.cpu().numpy(), lat.cpu().numpy(), nat))  # (numpy: see _parity_worker)
     finally:
         dist.destroy_process_group()
 
@@ -79,9 +79,9 @@ def test_two_ranks_match_single_process():
     assert nat1 == NAT
     for rank, a, x, lat, nat in res:
         assert nat == NAT, rank
-        assert torch.equal(a, a1.cpu()), f"rank {rank}: atom types differ"
-        assert torch.equal(x, x1.cpu()), f"rank {rank}: coordinates differ"
-        assert torch.equal(lat, l1.cpu()), f"rank {rank}: lattices differ"
+        assert torch.equal(torch.from_numpy(a), a1.cpu()), f"rank {rank}: atom types differ"
+        assert torch.equal(torch.from_numpy(x), x1.cpu()), f"rank {rank}: coordinates differ"
+        assert torch.equal(torch.from_numpy(lat), l1.cpu()), f"rank {rank}: lattices differ"
 
 
 def _parity_worker(rank, world, port, q, want):
@@ -104,7 +104,8 @@ def _parity_worker(rank, world, port, q, want):
                                                       every_step=want):
             if t in want:
                 got[t] = [v.cpu().numpy().copy() for v in (a, x, lat)]
-        gen_state = torch.get_rng_state()
+        # (numpy through the queue: a torch tensor travels as a shared fd that dies with this process)
+        gen_state = torch.get_rng_state().numpy().copy()
         # the drop-in call: sample() notices the process group and shards by itself
         torch.manual_seed(7)
         atoms = m.sample(None, 5, 6, text_embeds=cond.cuda(), null_text_embeds=null.cuda())
@@ -152,6 +153,6 @@ def test_two_ranks_parity_mode_64x20_trajectory(golden):
         for t in sorted(one):
             for k, what in enumerate(("atom types", "coordinates", "lattices")):
                 assert np.array_equal(got[t][k], one[t][k]), f"rank {rank}, t={t}: {what} differ from one process"
-        assert torch.equal(gen_state, gen_one), f"rank {rank}: CPU generator ends elsewhere than in one process"
+        assert np.array_equal(gen_state, gen_one.numpy()), f"rank {rank}: CPU generator ends elsewhere than in one process"
         assert summary == summary_one, f"rank {rank}: Chemeleon.sample() under 2 ranks differs from one process"
         gate_64x20(got, g, label=f"64x20 T=1000, 2 ranks (rank {rank})")
