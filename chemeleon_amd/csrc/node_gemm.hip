@@ -162,27 +162,34 @@ __device__ __forceinline__ void node_epilogue_split(const GemmArgs& g, f32x16 (&
 // PS (S16 only): A arrives pre-split (GemmArgs::aex): its fragments are read from LDS as they are, the
 // accumulators are rescaled by 2^(e_prev - e_next) where a 128-column chunk of K ends (exact), and the
 // epilogue can write C split the same way (GemmArgs::Cs).
-template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false>
+// NNT (split16, 64-row tiles only): tile columns, 128 or 64 (4 waves of 32x32: twice the blocks again, for
+// grids still short of the CUs). Every output element's K sum runs in the same order whatever the tile
+// shape, so all tilings are bit-identical.
+template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false, int NNT = 128>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4),
                 "tiling");
   static_assert(!PS || S16, "pre-split A is a split16 form");
+  static_assert(NNT == 128 || (NNT == 64 && S16 && !PS && NMT == 64), "64-column tiles: split16, 64 rows");
   constexpr int NM = NMT, NI = NMT / 64;  // tile rows; 32-row fragment groups per wave
+  constexpr int NJ = NNT / 64;            // 32-column fragment groups per wave
   constexpr int A_STB_ = A_STB<NMT>;
   // K-tiles in flight: all NST stages. Tile t's stage is read in step t-1 (read_raw(t)), so after
   // step t's barrier it takes tile t + NST while tiles t+1 .. t+NST-1 are in flight or landed.
-  constexpr int STB_ = STB<S16, NMT>, NST_ = NST<S16, NB, NMT>, AHEAD = NST_;
-  constexpr int GL = S16 ? 2 + NI : 5;                                   // glds per thread and K-tile
+  constexpr int STB_ = NNT == 128 ? STB<S16, NMT> : A_STB_ + NNT * 64;
+  constexpr int NST_ = NNT == 128 ? NST<S16, NB, NMT> : 4, AHEAD = NST_;
+  constexpr int NWI = S16 ? NNT / 64 : 3;                                // W glds per thread and K-tile
+  constexpr int GL = S16 ? NWI + NI : 5;                                 // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int h = lane >> 5, r32 = lane & 31;
-  const int ntn = g.N / NN;
+  const int ntn = g.N / NNT;
   // XCD-aware order (workgroups go round-robin to the 8 XCDs): each XCD takes a contiguous range of
   // tiles, so the column tiles of a row tile run on one XCD and read their A rows once from HBM
   // (without it every column tile fetched A again into another XCD's L2: 538 MB per launch vs 84-168)
   const long bid = g.linear_order ? (long)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  const int n0 = (int)(bid % ntn) * NN;
+  const int n0 = (int)(bid % ntn) * NNT;
   const long row0 = (bid / ntn) * NM;
   const long nrows = g.M - row0 < NM ? g.M - row0 : NM;
   const int nk = g.K / NK;
@@ -204,8 +211,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   // W (bf16x3): instruction q (of 12) is plane q >> 2, rows 32 (q & 3) + (L >> 1), LDS piece L & 1
   // holding logical piece (L & 1) ^ ((L >> 4) & 1); wave w issues q = 3w .. 3w + 2.
   // W (S16): rows of 64 B [hi 16 | lo 16] per K-tile, swizzled like A; instruction q (of 8) covers
-  // rows 16q + (L >> 2), LDS piece L & 3 holding logical piece alp; wave w issues q = 2w, 2w + 1.
-  constexpr int NWI = S16 ? 2 : 3;
+  // rows 16q + (L >> 2), LDS piece L & 3 holding logical piece alp; wave w issues q = NWI w .. NWI w + NWI-1.
   const int wlp = (lane & 1) ^ ((lane >> 4) & 1);
   const __bf16* Wpl = reinterpret_cast<const __bf16*>(g.Wp3);
   const long wplane = (long)g.N * g.K;
@@ -214,7 +220,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 #pragma unroll
   for (int u = 0; u < NWI; ++u) {
     if constexpr (S16) {
-      const int q = 2 * wave + u;
+      const int q = NWI * wave + u;
       wsrc[u] = Wpl + (long)(n0 + 16 * q + (lane >> 2)) * 2 * g.K + 8 * alp;
       wdst[u] = A_STB_ + q * 1024;
     } else {
@@ -236,11 +242,11 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
       __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + (S16 ? 2 * k0 : k0)), (lds_void*)(st + wdst[u]), 16, 0, 0);
   };
 
-  f32x16 acc[NI][2];
+  f32x16 acc[NI][NJ];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
@@ -283,8 +289,8 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   const int fa0 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h) ^ asw);
   const int fa1 = (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 * h + 1) ^ asw);
   const int fw = A_STB_ + (wn * 64 + r32) * W_ROWB + 16 * (h ^ wsw);
-  const int fw16[2] = {A_STB_ + (wn * 64 + r32) * 64 + 16 * (h ^ asw),         // hi piece h
-                       A_STB_ + (wn * 64 + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
+  const int fw16[2] = {A_STB_ + (wn * (NNT / 2) + r32) * 64 + 16 * (h ^ asw),         // hi piece h
+                       A_STB_ + (wn * (NNT / 2) + r32) * 64 + 16 * ((2 + h) ^ asw)};  // lo piece 2 + h
 
   // Software pipeline (VAR 0): while the 24 MFMAs of K-tile t run, the fragments of tile t+1 are
   // read from LDS and its A part is split, both interleaved between the MFMAs (the split's VALU
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   constexpr int NP = S16 ? 2 : 3;  // operand parts
   typedef std::conditional_t<S16, f16x8, bf16x8> frag;
   f32x4 ra0[NI], ra1[NI];
-  frag fa[2][NP][NI], fwt[2][NP][2];  // [set][part][i / j]
+  frag fa[2][NP][NI], fwt[2][NP][NJ];  // [set][part][i / j]
   // PS: the A fragments as they are (hi piece h, lo piece 2 + h of the row's 64-B K-tile, swizzled like W16)
   const int fa16[2] = {(wm * (NM / 2) + r32) * A_ROWB + 16 * (h ^ asw), (wm * (NM / 2) + r32) * A_ROWB + 16 * ((2 + h) ^ asw)};
   auto read_raw = [&](int t, int set) {
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
         fwt[set][p][j] = S16 ? *reinterpret_cast<const frag*>(st + fw16[p] + j * 32 * 64)
                              : *reinterpret_cast<const frag*>(st + fw + p * W_PLB + j * 32 * W_ROWB);
   };
@@ -352,7 +358,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           if constexpr (S16)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fwt[set][PW[k]][j], fa[set][PA[k]][i], acc[i][j], 0, 0, 0);
           else
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
         for (int i = 0; i < NI; ++i) {
           const float f = ldexpf(1.0f, chunk_e(i, c - 1) - chunk_e(i, c));
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] *= f;
+          for (int j = 0; j < NJ; ++j) acc[i][j] *= f;
         }
       }
     }
@@ -390,17 +396,18 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
     if constexpr (S16) {
-      mfmas(cur, 0, 1);                               // 2 NI MFMAs beside the 4 + 2 NI fragment reads
+      mfmas(cur, 0, 1);                               // NI NJ MFMAs beside the 2 NI + 2 NJ fragment reads
+      constexpr int MF1 = NI * NJ, RD1 = (2 * NI + 2 * NJ + MF1 - 1) / MF1;
 #pragma unroll
-      for (int k = 0; k < 2 * NI; ++k) {
+      for (int k = 0; k < MF1; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, NI == 2 ? 2 : 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, RD1, 0);
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       split(cur ^ 1);
-      mfmas(cur, 1, 3);                               // 4 NI MFMAs, the split's VALU between them
+      mfmas(cur, 1, 3);                               // 2 NI NJ MFMAs, the split's VALU between them
 #pragma unroll
-      for (int k = 0; k < 4 * NI; ++k) {
+      for (int k = 0; k < 2 * NI * NJ; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
         __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
       }
@@ -445,10 +452,10 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
       const long row = row0 + lr;
       const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int col = n0 + wn * 64 + j * 32 + 8 * q + 4 * h;
+          const int col = n0 + wn * (NNT / 2) + j * 32 + 8 * q + 4 * h;
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
@@ -500,6 +507,7 @@ hipError_t node_gemm_init() {
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
 int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
+int g_node_cols = 0;    // S16 64-row tile columns override (microbenchmarks): 0 = default, 64, 128
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
 // rows of 16-column chunks, g.wscale = their row scales)
@@ -532,6 +540,11 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
     } else {
       hipLaunchKernelGGL((k_node_gemm<0, true, 2, 128, true>), grid, block, NODE_LDS, s, g);
     }
+    return hipGetLastError();
+  }
+  if (g.wscale && rows == 64 && g_node_cols == 64) {
+    const dim3 grid6464((unsigned)(((g.M + 63) / 64) * (g.N / 64)));
+    hipLaunchKernelGGL((k_node_gemm<0, true, 4, 64, false, 64>), grid6464, block, 4 * (A_STB<64> + 64 * 64), s, g);
     return hipGetLastError();
   }
   if (g.wscale && rows == 64) {

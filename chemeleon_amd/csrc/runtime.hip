@@ -1287,7 +1287,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     }
     HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
   }
-  if (b->xbad && b->math == MATH_SPLIT16) {
+  // (edge layer 1 on pairs as two launches, the default: no intra-grid waits, nothing to clear; the three
+  // memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
+  const bool waits = !(pairs && !m->edge_pairs_layer);
+  if (b->xbad && b->math == MATH_SPLIT16 && waits) {
     // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[kMaxLayers + l])
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)

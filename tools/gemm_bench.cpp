@@ -169,6 +169,36 @@ int main(int argc, char** argv) {
     printf("empty kernel, 160 blocks: %.2f us per launch\n", te * 1e3);
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "node64") {  // short grids: 64x128 vs 64x64 split16 node tiles
+    CK(node_gemm_init());
+    void* W16; float* wsc16; float* amax;
+    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
+    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
+    std::vector<float> one(M, 1.0f);
+    CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
+    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax;
+    const size_t nc = (size_t)M * N;
+    std::vector<float> c0(nc), c1(nc);
+    for (int rep = 0; rep < 2; ++rep) {
+      float t[3];
+      const int cols[3] = {128, 64, 128};
+      for (int v = 0; v < 3; ++v) {
+        g_node_rows = 64; g_node_blocks = 3; g_node_cols = cols[v];
+        t[v] = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+      }
+      g_node_rows = 64; g_node_blocks = 3; g_node_cols = 128;
+      CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(c0.data(), C, nc * 4, hipMemcpyDeviceToHost));
+      CK(hipMemset(C, 0, nc * 4));
+      g_node_cols = 64;
+      CK(node_gemm(g16, s)); CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(c1.data(), C, nc * 4, hipMemcpyDeviceToHost));
+      g_node_rows = 0; g_node_blocks = 0; g_node_cols = 0;
+      printf("M=%ld N=%d K=%d: 64x128 tiles %.2f us | 64x64 tiles %.2f us | 64x128 again %.2f us | bit-identical: %s\n",
+             M, N, K, t[0] * 1e3, t[1] * 1e3, t[2] * 1e3, c0 == c1 ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
     CK(node_gemm_init());
     for (int rep = 0; rep < 2; ++rep) {
