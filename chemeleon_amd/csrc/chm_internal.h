@@ -198,8 +198,10 @@ struct PairSched {
   long R;
   int skip_x;          // (tests) the blocks on this XCD exit at once: the launch's self-check must catch it
 };
+// persistent: k_edge16_pairs_layer (a job loop per block, grid = CUs); else k_edge16_pairs_grid (static grid of
+// 8 x jstride blocks, block 8 k + x = job k of XCD x)
 hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
-                                   int repair_grid, hipStream_t s);
+                                   int repair_grid, hipStream_t s, bool persistent);
 // (host) XCD job lists of k_edge16_pairs_layer for an fc batch: row tiles' pair-tile ranges, per XCD its first
 // pair tile and job list (lag in pair tiles)
 struct PairPlan {

@@ -1520,8 +1520,51 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_layer(EdgeArgs g1, Edge
   }
 }
 
+// The static-grid form (option edge_pairs_layer = 1): block 8 k + x runs job k of XCD x's list (pair_plan),
+// one tile per block, no job loop. Workgroups are dispatched in index order and round-robin over the XCDs,
+// so block 8 k + x runs on XCD x and every pair tile a layer-2 job waits for belongs to an earlier block of
+// the same XCD: dispatched before it, never waiting itself. A pair tile that ran on another XCD than
+// planned marks its flag (bits 16+), and a layer-2 job that finds such a flag, runs on another XCD itself
+// or times out raises the layer's repair request (the repair launches behind the grid recompute the layer).
+__global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeArgs g2, PairSched ps) {
+  const int xs = (int)(blockIdx.x & 7u), k = (int)(blockIdx.x >> 3);
+  if (k >= ps.njobs[xs]) return;
+  const int2 j = ps.jobs[(long)xs * ps.jstride + k];
+  const unsigned me = xcc_id();
+  if (j.x == 1) {
+    pair_tile(g1, j.y, threadIdx.x);
+    // every store of this tile has reached the XCD's L2; count the column tile (and a misplaced block)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(ps.pflag + (long)xs * ps.npx + (j.y / 2 - ps.pa[xs]), me == (unsigned)xs ? 1u : 0x10001u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (j.x != 2) return;
+  if (threadIdx.x == 0) {  // wait (bounded) until both column tiles of every pair tile read are in
+    const int2 r = ps.rng[j.y / (2 * g2.npairs)];
+    bool late = false, other = me != (unsigned)xs;
+    for (int p = r.x; p <= r.y && !late; ++p) {
+      const unsigned* f = ps.pflag + (long)xs * ps.npx + (p - ps.pa[xs]);
+      unsigned v, spins = 0;
+      while (((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffu) < 2u &&
+             ++spins < (1u << 21))
+        __builtin_amdgcn_s_sleep(4);
+      late = (v & 0xffffu) < 2u;
+      other |= (v >> 16) != 0u;
+    }
+    if (late || other || (g2.dbg & 512))  // (dbg 512, tests: option edge_layer_repair)
+      __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (late) count_event(EV_LAYER_TIMEOUT);
+    else if (other) count_event(EV_LAYER_XCD);
+  }
+  __syncthreads();
+  edge16_tile<EPI_SEGMEAN, true>(g2, 0, 0, j.y);
+}
+
 hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
-                                   int repair_grid, hipStream_t s) {
+                                   int repair_grid, hipStream_t s, bool persistent) {
   if (g1.N != H || g1.K != FD || !g1.A || !g1.W || !g1.wscale || !g1.S || !g1.sexp || !g1.PQ || !g1.pi || !g1.pj ||
       !g1.pe || g1.Mp < 1 || g1.npairs != g2.npairs || g1.E < g1.Mp || !g1.xbad || g1.xbad != g2.xbad)
     return hipErrorInvalidValue;
@@ -1532,7 +1575,10 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
   if (!ps.jobs || !ps.njobs || !ps.rng || !ps.pa || !ps.cnt || !ps.pflag || !ps.done || grid < 1)
     return hipErrorInvalidValue;
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_edge16_pairs_layer, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, ps);
+  if (persistent)
+    hipLaunchKernelGGL(k_edge16_pairs_layer, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, ps);
+  else
+    hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (g1.dbg & 16384)) return e;  // (dbg 16384: profiling / tests, no repair launches)
   // the repair launches (exit at once unless a wait timed out or layer-2 jobs are missing): clear layer 2's
@@ -1555,7 +1601,8 @@ static hipError_t edge16_init_once() {
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
-                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_layer};
+                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_layer,
+                      (const void*)k_edge16_pairs_grid};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;

@@ -88,8 +88,8 @@ struct chm_model {
   int edge_pairs = 1;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
   int edge_pairs_layer = 0;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
-                             // persistent grid (k_edge16_pairs_layer). Experimental, off: its first GPU run
-                             // faulted (DESIGN.md §4 "Edge layer 1 on pairs"); the two-launch form is validated
+                             // grid: 1 = static grid (k_edge16_pairs_grid), 2 = persistent job loop
+                             // (k_edge16_pairs_layer, experimental: its first GPU run faulted)
   int ncu = 0;          // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
@@ -489,8 +489,9 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_pairs = value != 0;
     return CHM_OK;
   }
-  if (k == "edge_pairs_layer") {  // (experimental, off) both edge layers on pairs in one grid (k_edge16_pairs_layer)
-    m->edge_pairs_layer = value != 0;
+  if (k == "edge_pairs_layer") {  // both edge layers on pairs in one grid: 0 off, 1 static grid, 2 persistent
+    if (value < 0 || value > 2) return fail(CHM_E_ARG, "edge_pairs_layer must be 0, 1 or 2");
+    m->edge_pairs_layer = (int)value;
     return CHM_OK;
   }
   if (k == "edge_lag") {
@@ -1368,7 +1369,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         ps.npx = b->pplan.npx; ps.cnt = w; ps.done = reinterpret_cast<unsigned long long*>(w + 8);
         ps.pflag = w + 16; ps.R = b->nrt; ps.skip_x = m->edge_skip_xcd;
         ProfScope ps_(CHM_K_EDGE_LAYER, s);
-        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->ncu, m->repair_grid, s));
+        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->ncu, m->repair_grid, s, m->edge_pairs_layer == 2));
       } else if (pairs) {
         // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
         EdgeArgs e1p = e1;

@@ -887,8 +887,44 @@ def test_edge_pairs_layer2_schedules_are_bit_identical(cn, nat):
             assert torch.equal(u, v), f"{what}: edge-pairs layer-2 schedule {k} differs"
 
 
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [40] * 512])
+def test_edge_pairs_grid_is_bit_identical(cn, nat):
+    """Both edge layers on pairs in one static grid (k_edge16_pairs_grid, option edge_pairs_layer = 1): block
+    8 k + x runs job k of XCD x's list, layer-2 jobs wait on per-pair-tile flags of their XCD. One reverse step
+    equals the two-launch pair schedule bit for bit, also with the repair launches forced
+    ('edge_layer_repair'); in the plain run no wait times out, no block runs on an unplanned XCD, nothing is
+    repaired."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(19)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    model.decoder.set_option("edge_pairs", 1)
+    model.decoder.set_option("edge_layer_min", 1)  # (the one-grid form for every shape here)
+    outs, events = [], []
+    for form, repair in ((0, 0), (1, 0), (1, 1)):
+        model.decoder.set_option("edge_pairs_layer", form)
+        model.decoder.set_option("edge_layer_repair", repair)
+        _lib.prof_events(reset=True)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+        torch.cuda.synchronize()
+        events.append(_lib.prof_events())
+    del model
+    torch.cuda.empty_cache()
+    print("events (two launches, static grid, forced repair):", events)
+    assert events[1]["layer_wait_timeouts"] == 0 and events[1]["layer_other_xcd"] == 0
+    assert events[1]["layer_repairs"] == 0
+    assert events[2]["layer_repairs"] == 12  # 2 decoder pairs x 6 layers
+    for k, name in ((1, "static grid"), (2, "static grid + forced repair")):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: {name} differs from the two-launch pair schedule"
+
+
 @pytest.mark.skipif(os.environ.get("CHM_TEST_PAIRS_LAYER") != "1",
-                    reason="experimental k_edge16_pairs_layer (option edge_pairs_layer, off): its first GPU run "
+                    reason="experimental k_edge16_pairs_layer (option edge_pairs_layer = 2): its first GPU run "
                            "faulted; set CHM_TEST_PAIRS_LAYER=1 to run it")
 @pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [40] * 512])
 def test_edge_pairs_one_grid_is_bit_identical(cn, nat):
@@ -907,7 +943,7 @@ def test_edge_pairs_one_grid_is_bit_identical(cn, nat):
           torch.randn(N, 3, generator=g))
     model = _model(1000)
     model.decoder.set_option("edge_pairs", 1)
-    model.decoder.set_option("edge_pairs_layer", 1)
+    model.decoder.set_option("edge_pairs_layer", 2)
     model.decoder.set_option("edge_layer_min", 1)  # (the one-grid form for every shape here)
     outs, events = [], []
     for layer, repair, skip in ((0, 0, -1), (1, 0, -1), (1, 1, -1), (1, 0, 3)):
