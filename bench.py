@@ -116,6 +116,15 @@ def edge_pairs_on():
     return os.environ.get("CHM_EDGE_PAIRS", "1") != "0"
 
 
+EDGE_PAIRS_LAYER_DEFAULT = "0"  # (the library's default of option edge_pairs_layer)
+
+
+def pairs_layer_kernel():
+    """The one-grid kernel of both edge layers on pairs (option edge_pairs_layer: 1 static grid, 2 persistent)."""
+    mode = os.environ.get("CHM_EDGE_PAIRS_LAYER", EDGE_PAIRS_LAYER_DEFAULT)
+    return {"1": "k_edge16_pairs_grid", "2": "k_edge16_pairs_layer"}.get(mode)
+
+
 def decoder_pair_flops(natoms, P=2, share_fourier=True, pairs=None):
     """Algorithmic fp32 flops of one decoder call pair as implemented
     (SURVEY.md §8(d) factorised formula, with the Fourier projection shared
@@ -557,7 +566,8 @@ def main():
     fou_flops = 2.0 * (Ep if edge_pairs_on() else E) * 768 * H  # edge layer 1: D.f once for both conditionings
     # (on pairs: once per unordered pair, k_edge16_pairs)
     fou_tflops = fou_flops / (ms_fou / nfou * 1e-3) / 1e12 if nfou else None
-    msg_kernel = ("k_edge16_pairs_layer" if edge_pairs_on() else "k_edge16_layer") if nlay else "k_edge16<2"
+    msg_kernel = ((pairs_layer_kernel() or "k_edge16_pairs") if edge_pairs_on() else "k_edge16_layer") if nlay \
+        else "k_edge16<2"
     traffic, traffic_src = None, "not collected for the ragged workload" if args.ragged else "not collected"
     if math == "split16" and not args.ragged:
         if rank == 0 and world == 1 and not args.no_traffic:
@@ -632,8 +642,8 @@ def main():
         "roofline": {"bound": "mfma",
                      "timing": ("HIP events on the launch stream, eager pass of 2 steps after the timed graph replays"
                                 if not args.no_graph else "HIP events on the launch stream over warm-up + timed steps"),
-                     "kernel": {"split16": (("both edge layers of a CSP layer in one persistent grid, layer 1 on "
-                                             "unordered pairs (k_edge16_pairs_layer: D.f once per pair i <= j, both "
+                     "kernel": {"split16": ((f"both edge layers of a CSP layer in one grid, layer 1 on "
+                                             f"unordered pairs ({msg_kernel}: D.f once per pair i <= j, both "
                                              "directions' S = SiLU(U +- V + P + Q); S.W2^T + SiLU + fused "
                                              "scatter_mean; 16x16x32 MFMA), both conditionings, incl. its three repair "
                                              "launches (no-ops unless a check fails)") if edge_pairs_on() else

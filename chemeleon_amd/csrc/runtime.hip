@@ -1356,8 +1356,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+      // (the static grid packs the two layers' tiles into one launch, which pays most on short grids: from 8
+      // row tiles on; the persistent form from edge_layer_min)
       if (pairs && m->edge_pairs_layer && e2.rtiles && m->edge_layer && b->psched && P == b->P &&
-          b->nrt >= m->edge_layer_min &&
+          b->nrt >= (m->edge_pairs_layer == 1 ? 8 : m->edge_layer_min) &&
           m->ncu > 0 && m->xcd_mask == 0xffu) {
         // both edge layers in one persistent grid, layer 1 on pairs (k_edge16_pairs_layer)
         EdgeArgs e1p = e1;
