@@ -542,7 +542,10 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
     }
     return hipGetLastError();
   }
-  if (g.wscale && rows == 64 && g_node_cols == 64) {
+  // 64x64 tiles where even the 64x128 grid is short of one block per CU (M = 2560, N = 512: 17.3 -> 15.3 us
+  // at K = 512, 28.3 -> 25.7 at K = 1024; from 256 blocks on they lose: profiles/r5/node/node64.txt)
+  const bool cols64 = g_node_cols ? g_node_cols == 64 : ((g.M + 63) / 64) * (g.N / NN) < 256;
+  if (g.wscale && rows == 64 && cols64 && !g.aex) {
     const dim3 grid6464((unsigned)(((g.M + 63) / 64) * (g.N / 64)));
     hipLaunchKernelGGL((k_node_gemm<0, true, 4, 64, false, 64>), grid6464, block, 4 * (A_STB<64> + 64 * 64), s, g);
     return hipGetLastError();
