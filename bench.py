@@ -116,7 +116,7 @@ def edge_pairs_on():
     return os.environ.get("CHM_EDGE_PAIRS", "1") != "0"
 
 
-EDGE_PAIRS_LAYER_DEFAULT = "0"  # (the library's default of option edge_pairs_layer)
+EDGE_PAIRS_LAYER_DEFAULT = "1"  # (the library's default of option edge_pairs_layer)
 
 
 def pairs_layer_kernel():

@@ -1520,12 +1520,13 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_layer(EdgeArgs g1, Edge
   }
 }
 
-// The static-grid form (option edge_pairs_layer = 1): block 8 k + x runs job k of XCD x's list (pair_plan),
-// one tile per block, no job loop. Workgroups are dispatched in index order and round-robin over the XCDs,
-// so block 8 k + x runs on XCD x and every pair tile a layer-2 job waits for belongs to an earlier block of
-// the same XCD: dispatched before it, never waiting itself. A pair tile that ran on another XCD than
-// planned marks its flag (bits 16+), and a layer-2 job that finds such a flag, runs on another XCD itself
-// or times out raises the layer's repair request (the repair launches behind the grid recompute the layer).
+// The static-grid form (option edge_pairs_layer = 1): block 8 k + x runs job k of list x (pair_plan), one
+// tile per block, no job loop. Workgroups are dispatched in index order and round-robin over the XCDs, so
+// the blocks of list x share one XCD (which one depends on where the dispatcher's rotation stands: measured
+// under graph replay, it is not always x) and every pair tile a layer-2 job waits for belongs to an earlier
+// block of the same list: dispatched before it, never waiting itself. Each column tile of a pair tile adds
+// 1 + (its XCD + 1) << (8 + 4 col) to its flag; a layer-2 job that finds another XCD there (S written through
+// another L2) or times out raises the layer's repair request (the repair launches recompute the layer).
 __global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeArgs g2, PairSched ps) {
   const int xs = (int)(blockIdx.x & 7u), k = (int)(blockIdx.x >> 3);
   if (k >= ps.njobs[xs]) return;
@@ -1537,22 +1538,22 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(ps.pflag + (long)xs * ps.npx + (j.y / 2 - ps.pa[xs]), me == (unsigned)xs ? 1u : 0x10001u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ps.pflag + (long)xs * ps.npx + (j.y / 2 - ps.pa[xs]),
+                             1u + ((me + 1u) << (8 + 4 * (j.y & 1))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if (j.x != 2) return;
   if (threadIdx.x == 0) {  // wait (bounded) until both column tiles of every pair tile read are in
     const int2 r = ps.rng[j.y / (2 * g2.npairs)];
-    bool late = false, other = me != (unsigned)xs;
+    bool late = false, other = false;
     for (int p = r.x; p <= r.y && !late; ++p) {
       const unsigned* f = ps.pflag + (long)xs * ps.npx + (p - ps.pa[xs]);
       unsigned v, spins = 0;
-      while (((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffu) < 2u &&
+      while (((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffu) < 2u &&
              ++spins < (1u << 21))
         __builtin_amdgcn_s_sleep(4);
-      late = (v & 0xffffu) < 2u;
-      other |= (v >> 16) != 0u;
+      late = (v & 0xffu) < 2u;
+      other |= ((v >> 8) & 15u) != me + 1u || ((v >> 12) & 15u) != me + 1u;
     }
     if (late || other || (g2.dbg & 512))  // (dbg 512, tests: option edge_layer_repair)
       __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

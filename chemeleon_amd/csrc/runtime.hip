@@ -87,9 +87,10 @@ struct chm_model {
   int edge_pool = 15;    // CHM_EDGE_POOL: the persistent form's run-time-claimed share of the row tiles (%)
   int edge_pairs = 1;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
-  int edge_pairs_layer = 0;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
-                             // grid: 1 = static grid (k_edge16_pairs_grid), 2 = persistent job loop
-                             // (k_edge16_pairs_layer, experimental: its first GPU run faulted)
+  int edge_pairs_layer = 1;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
+                             // grid from edge_layer_min row tiles on: 1 = static grid (k_edge16_pairs_grid), 2 =
+                             // persistent job loop (k_edge16_pairs_layer, experimental: its first GPU run faulted,
+                             // DESIGN.md §4), 0 = two launches
   int ncu = 0;          // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
@@ -1290,17 +1291,19 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   }
   // (edge layer 1 on pairs as two launches, the default: no intra-grid waits, nothing to clear; the three
   // memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
-  const bool waits = !(pairs && !m->edge_pairs_layer);
+  // both edge layers on pairs in one grid (k_edge16_pairs_grid / _layer) for this call
+  const bool pair_grid = pairs && m->edge_pairs_layer && m->edge_rows && b->rtiles && m->edge_layer && b->psched &&
+                         P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu;
+  const bool waits = !pairs || pair_grid;
   if (b->xbad && b->math == MATH_SPLIT16 && waits) {
     // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[kMaxLayers + l])
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)
     HIPCHK(hipMemsetAsync(b->xbad, 0, 2 * kMaxLayers * sizeof(unsigned), s));
-    if (m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
+    if (!pairs && m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
-    if (m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
-    if (b->psched && m->edge_pairs && m->edge_pairs_layer && m->edge_layer)
-      HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned), s));
+    if (!pairs && m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
+    if (pair_grid) HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
@@ -1356,12 +1359,10 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
       const bool instrumented = g_prof_on && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
-      // (the static grid packs the two layers' tiles into one launch, which pays most on short grids: from 8
-      // row tiles on; the persistent form from edge_layer_min)
-      if (pairs && m->edge_pairs_layer && e2.rtiles && m->edge_layer && b->psched && P == b->P &&
-          b->nrt >= (m->edge_pairs_layer == 1 ? 8 : m->edge_layer_min) &&
-          m->ncu > 0 && m->xcd_mask == 0xffu) {
-        // both edge layers in one persistent grid, layer 1 on pairs (k_edge16_pairs_layer)
+      // (same-box A/B, static grid against two launches: 64x40 8.47 -> 7.77 ms per step, 512x40 54.9 -> 54.8,
+      // 64x20 2.95 -> 3.10: 100 row tiles leave each XCD's job list too short to pack; profiles/r5/grid/)
+      if (pair_grid) {
+        // both edge layers in one grid, layer 1 on pairs (k_edge16_pairs_grid, or the persistent k_edge16_pairs_layer)
         EdgeArgs e1p = e1;
         e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
         e1p.xbad = e2.xbad = b->xbad + l;

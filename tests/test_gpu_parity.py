@@ -889,8 +889,9 @@ def test_edge_pairs_layer2_schedules_are_bit_identical(cn, nat):
 
 @pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [40] * 512])
 def test_edge_pairs_grid_is_bit_identical(cn, nat):
-    """Both edge layers on pairs in one static grid (k_edge16_pairs_grid, option edge_pairs_layer = 1): block
-    8 k + x runs job k of XCD x's list, layer-2 jobs wait on per-pair-tile flags of their XCD. One reverse step
+    """Both edge layers on pairs in one static grid (k_edge16_pairs_grid, option edge_pairs_layer = 1, the default
+    from 256 row tiles): block 8 k + x runs job k of list x, layer-2 jobs wait on per-pair-tile flags of their
+    list (3 row tiles here too: lists of XCDs without rows are empty). One reverse step
     equals the two-launch pair schedule bit for bit, also with the repair launches forced
     ('edge_layer_repair'); in the plain run no wait times out, no block runs on an unplanned XCD, nothing is
     repaired."""
