@@ -120,9 +120,9 @@ EDGE_PAIRS_LAYER_DEFAULT = "1"  # (the library's default of option edge_pairs_la
 
 
 def pairs_layer_kernel():
-    """The one-grid kernel of both edge layers on pairs (option edge_pairs_layer: 1 static grid, 2 persistent)."""
+    """The one-grid kernel of both edge layers on pairs (option edge_pairs_layer, 0 = two launches)."""
     mode = os.environ.get("CHM_EDGE_PAIRS_LAYER", EDGE_PAIRS_LAYER_DEFAULT)
-    return {"1": "k_edge16_pairs_grid", "2": "k_edge16_pairs_layer"}.get(mode)
+    return None if mode == "0" else "k_edge16_pairs_grid"
 
 
 def decoder_pair_flops(natoms, P=2, share_fourier=True, pairs=None):

@@ -190,18 +190,14 @@ struct PairSched {
   const int* njobs;    // [8]
   int jstride;
   const int2* rng;     // [R] the pair tiles [lo, hi] row tile t reads
-  const int* pa;       // [8] XCD x's first pair tile
-  int npx;             // pflag entries per XCD
-  unsigned* cnt;       // [8]
-  unsigned* pflag;     // [8][npx]
-  unsigned long long* done;
+  const int* pa;       // [8] list x's first pair tile
+  int npx;             // pflag entries per list
+  unsigned* pflag;     // [8][npx]: finished column tiles | their XCD + 1 << (8 + 4 col)
   long R;
-  int skip_x;          // (tests) the blocks on this XCD exit at once: the launch's self-check must catch it
 };
-// persistent: k_edge16_pairs_layer (a job loop per block, grid = CUs); else k_edge16_pairs_grid (static grid of
-// 8 x jstride blocks, block 8 k + x = job k of XCD x)
-hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
-                                   int repair_grid, hipStream_t s, bool persistent);
+// k_edge16_pairs_grid: static grid of 8 x jstride blocks, block 8 k + x = job k of list x, then the repair launches
+hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int repair_grid,
+                                   hipStream_t s);
 // (host) XCD job lists of k_edge16_pairs_layer for an fc batch: row tiles' pair-tile ranges, per XCD its first
 // pair tile and job list (lag in pair tiles)
 struct PairPlan {

@@ -1385,12 +1385,12 @@ hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Both edge layers of a CSP layer in one persistent grid, edge layer 1 on pairs (chm_internal.h PairSched).
-// The directed one-grid kernel (k_edge16_layer_dyn) pairs layer-1 row tile t with layer-2 row tile t; on pairs,
+// Both edge layers of a CSP layer in one grid, edge layer 1 on pairs (chm_internal.h PairSched).
+// The directed one-grid kernels (k_edge16_layer*) pair layer-1 row tile t with layer-2 row tile t; on pairs,
 // layer-2 row tile t reads the S rows of every pair tile of its crystals up to its last node's pair row, a
 // contiguous range [lo(t), hi(t)] (pair_plan). Each XCD runs a contiguous range of row tiles and all the pair
-// tiles they read, so every S row a layer-2 tile reads was written through the same XCD's L2. Ranges of
-// neighbouring XCDs may share a pair tile: both compute it and write identical bytes.
+// tiles they read, so every S row a layer-2 tile reads was written through the same XCD's L2 (list x = the
+// jobs of one XCD). Ranges of neighbouring lists may share a pair tile: both compute it and write identical bytes.
 void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int lag, PairPlan& out) {
   const int B = (int)nat.size();
   std::vector<long> eoff(B + 1, 0), poff(B + 1, 0);
@@ -1445,81 +1445,6 @@ void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int 
   for (int x = 0; x < 8; ++x) std::copy(jl[x].begin(), jl[x].end(), out.jobs.begin() + (size_t)x * out.jstride);
 }
 
-__global__ __launch_bounds__(512, 1) void k_edge16_pairs_layer(EdgeArgs g1, EdgeArgs g2, PairSched ps) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const unsigned x = xcc_id();
-  const int P = g2.npairs;
-  int* bc = reinterpret_cast<int*>(lds);
-  for (;;) {
-    if (threadIdx.x == 0) {
-      int code = 0, idx = 0;
-      if ((int)x != ps.skip_x) {
-        const unsigned k = __hip_atomic_fetch_add(ps.cnt + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((int)k < ps.njobs[x]) {
-          const int2 j = ps.jobs[(long)x * ps.jstride + k];
-          code = j.x;
-          idx = j.y;
-          if (code == 2) {  // wait (bounded) until this XCD has finished both column tiles of every pair tile read
-            const int2 r = ps.rng[idx / (2 * P)];
-            bool late = false;
-            for (int p = r.x; p <= r.y && !late; ++p) {
-              const unsigned* f = ps.pflag + (long)x * ps.npx + (p - ps.pa[x]);
-              unsigned spins = 0;
-              while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 2u && ++spins < (1u << 21))
-                __builtin_amdgcn_s_sleep(4);
-              late = spins >= (1u << 21);
-            }
-            if (late) {  // (never in a healthy run: the layer is recomputed by the repair launches)
-              __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              count_event(EV_LAYER_TIMEOUT);
-            }
-          }
-        }
-      }
-      if (code == 0) {  // exit; the last block out checks that every layer-2 job ran (the 8-XCD assumption)
-        const unsigned long long old = __hip_atomic_fetch_add(ps.done, 1ull << 32, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-        if ((old >> 32) + 1ull == (unsigned long long)gridDim.x) {
-          if ((old & 0xffffffffull) != (unsigned long long)ps.R * P * 2) {
-            __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            count_event(EV_LAYER_INCOMPLETE);
-          } else if (g2.dbg & 512) {  // (tests, option edge_layer_repair: the repair launches always run)
-            __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      }
-      bc[0] = code;
-      bc[1] = idx;
-    }
-    __syncthreads();
-    const int code = bc[0], idx = bc[1];
-    __syncthreads();
-    if (code == 0) break;
-    // (laundered kernarg pointers, as k_edge16_layer_dyn: the tiles read their arguments from memory)
-    typedef const __attribute__((address_space(4))) char* kptr;
-    kptr kp = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(kp));
-    constexpr long off2 = (sizeof(EdgeArgs) + alignof(EdgeArgs) - 1) / alignof(EdgeArgs) * alignof(EdgeArgs);
-    const EdgeArgs* a1 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)kp;
-    const EdgeArgs* a2 = (const EdgeArgs*)(const __attribute__((address_space(4))) EdgeArgs*)(kp + off2);
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));
-    if (code == 1) {
-      pair_tile(*a1, idx, tid);
-      // every store of this tile has reached the XCD's L2; count the column tile
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0)
-        __hip_atomic_fetch_add(ps.pflag + (long)x * ps.npx + (idx / 2 - ps.pa[x]), 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      edge16_tile<EPI_SEGMEAN, true>(*a2, 0, 0, idx, tid);
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // The static-grid form (option edge_pairs_layer = 1): block 8 k + x runs job k of list x (pair_plan), one
 // tile per block, no job loop. Workgroups are dispatched in index order and round-robin over the XCDs, so
 // the blocks of list x share one XCD (which one depends on where the dispatcher's rotation stands: measured
@@ -1564,8 +1489,8 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeA
   edge16_tile<EPI_SEGMEAN, true>(g2, 0, 0, j.y);
 }
 
-hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int grid,
-                                   int repair_grid, hipStream_t s, bool persistent) {
+hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int repair_grid,
+                                   hipStream_t s) {
   if (g1.N != H || g1.K != FD || !g1.A || !g1.W || !g1.wscale || !g1.S || !g1.sexp || !g1.PQ || !g1.pi || !g1.pj ||
       !g1.pe || g1.Mp < 1 || g1.npairs != g2.npairs || g1.E < g1.Mp || !g1.xbad || g1.xbad != g2.xbad)
     return hipErrorInvalidValue;
@@ -1573,13 +1498,10 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
       !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags ||
       (long)g2.ntiles != ps.R || (long)g2.ntiles * BM < g2.E)
     return hipErrorInvalidValue;
-  if (!ps.jobs || !ps.njobs || !ps.rng || !ps.pa || !ps.cnt || !ps.pflag || !ps.done || grid < 1)
+  if (!ps.jobs || !ps.njobs || !ps.rng || !ps.pa || !ps.pflag)
     return hipErrorInvalidValue;
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
-  if (persistent)
-    hipLaunchKernelGGL(k_edge16_pairs_layer, dim3((unsigned)grid), dim3(512), LDS_B, s, g1, g2, ps);
-  else
-    hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
+  hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (g1.dbg & 16384)) return e;  // (dbg 16384: profiling / tests, no repair launches)
   // the repair launches (exit at once unless a wait timed out or layer-2 jobs are missing): clear layer 2's
@@ -1602,8 +1524,7 @@ static hipError_t edge16_init_once() {
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
-                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_layer,
-                      (const void*)k_edge16_pairs_grid};
+                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_grid};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;

@@ -88,9 +88,7 @@ struct chm_model {
   int edge_pairs = 1;    // CHM_EDGE_PAIRS / option edge_pairs: fc edge layer 1 on unordered pairs (k_edge16_pairs:
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
   int edge_pairs_layer = 1;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
-                             // grid from edge_layer_min row tiles on: 1 = static grid (k_edge16_pairs_grid), 2 =
-                             // persistent job loop (k_edge16_pairs_layer, experimental: its first GPU run faulted,
-                             // DESIGN.md §4), 0 = two launches
+                             // static grid (k_edge16_pairs_grid) from edge_layer_min row tiles on; 0 = two launches
   int ncu = 0;          // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
@@ -490,9 +488,8 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_pairs = value != 0;
     return CHM_OK;
   }
-  if (k == "edge_pairs_layer") {  // both edge layers on pairs in one grid: 0 off, 1 static grid, 2 persistent
-    if (value < 0 || value > 2) return fail(CHM_E_ARG, "edge_pairs_layer must be 0, 1 or 2");
-    m->edge_pairs_layer = (int)value;
+  if (k == "edge_pairs_layer") {  // both edge layers on pairs in one static grid (k_edge16_pairs_grid): 1 on, 0 off
+    m->edge_pairs_layer = value != 0;
     return CHM_OK;
   }
   if (k == "edge_lag") {
@@ -761,7 +758,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->prng = (int2*)carve(b->pplan.rng.size() * sizeof(int2));
     b->pnjobs = (int*)carve(8 * sizeof(int));
     b->ppa = (int*)carve(8 * sizeof(int));
-    b->psched = (unsigned*)carve((size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned));
+    b->psched = (unsigned*)carve((size_t)L * 8 * b->pplan.npx * sizeof(unsigned));
   }
   if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
     b->rtiles = (int4*)carve(b->nrt * sizeof(int4));
@@ -1291,7 +1288,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   }
   // (edge layer 1 on pairs as two launches, the default: no intra-grid waits, nothing to clear; the three
   // memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
-  // both edge layers on pairs in one grid (k_edge16_pairs_grid / _layer) for this call
+  // both edge layers on pairs in one grid (k_edge16_pairs_grid) for this call
   const bool pair_grid = pairs && m->edge_pairs_layer && m->edge_rows && b->rtiles && m->edge_layer && b->psched &&
                          P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu;
   const bool waits = !pairs || pair_grid;
@@ -1303,7 +1300,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     if (!pairs && m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (!pairs && m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
-    if (pair_grid) HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * (16 + 8 * b->pplan.npx) * sizeof(unsigned), s));
+    if (pair_grid) HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * 8 * b->pplan.npx * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
@@ -1362,17 +1359,15 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       // (same-box A/B, static grid against two launches: 64x40 8.47 -> 7.77 ms per step, 512x40 54.9 -> 54.8,
       // 64x20 2.95 -> 3.10: 100 row tiles leave each XCD's job list too short to pack; profiles/r5/grid/)
       if (pair_grid) {
-        // both edge layers in one grid, layer 1 on pairs (k_edge16_pairs_grid, or the persistent k_edge16_pairs_layer)
+        // both edge layers in one grid, layer 1 on pairs (k_edge16_pairs_grid)
         EdgeArgs e1p = e1;
         e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
         e1p.xbad = e2.xbad = b->xbad + l;
         PairSched ps;
-        unsigned* w = b->psched + (size_t)l * (16 + 8 * b->pplan.npx);
         ps.jobs = b->pjobs; ps.njobs = b->pnjobs; ps.jstride = b->pplan.jstride; ps.rng = b->prng; ps.pa = b->ppa;
-        ps.npx = b->pplan.npx; ps.cnt = w; ps.done = reinterpret_cast<unsigned long long*>(w + 8);
-        ps.pflag = w + 16; ps.R = b->nrt; ps.skip_x = m->edge_skip_xcd;
+        ps.npx = b->pplan.npx; ps.pflag = b->psched + (size_t)l * 8 * b->pplan.npx; ps.R = b->nrt;
         ProfScope ps_(CHM_K_EDGE_LAYER, s);
-        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->ncu, m->repair_grid, s, m->edge_pairs_layer == 2));
+        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->repair_grid, s));
       } else if (pairs) {
         // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
         EdgeArgs e1p = e1;

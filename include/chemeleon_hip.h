@@ -87,14 +87,17 @@ void chm_model_destroy(chm_model* m);
  *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag", "edge_layer_min": edge-layer
  *     schedules (bit-identical).
  *   "node_ps" (0 / 1): split16 node GEMMs read their A operands pre-split by the producing kernels (not
- *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs");
- *   "edge_pairs" (0 / 1): fc edge layer 1 computed once per unordered pair of atoms (the reverse edge's
- *     Fourier features are the forward ones with the sine half negated), both directions' messages from one
- *     GEMM row; within fp32 rounding of the directed form (DESIGN.md §4 "Edge layer 1 on pairs"); a batch carves their buffers only
- *     when created while the option is set (batches created without it keep the in-loop split). The persistent one-grid kernel (edge_layer_dyn) runs only where
- *     model creation saw 8 XCDs ("xcd_mask" = 0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD
- *     exit, the launch's self-check must raise the repair), "edge_layer_repair", "edge_tail_timeout",
- *     "edge_tail_norepair" (WRONG results after a timeout), "edge_rows_nowait".
+ *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs"); a batch carves their buffers only
+ *     when created while the option is set (batches created without it keep the in-loop split).
+ *   "edge_pairs" (0 / 1, default 1): fc edge layer 1 computed once per unordered pair of atoms (the reverse
+ *     edge's Fourier features are the forward ones with the sine half negated), both directions' messages
+ *     from one GEMM row; within fp32 rounding of the directed form (DESIGN.md §4 "Edge layer 1 on pairs").
+ *   "edge_pairs_layer" (0 / 1, default 1): with edge_pairs, both edge layers in one static grid from
+ *     "edge_layer_min" row tiles on (k_edge16_pairs_grid; bit-identical to two launches).
+ *   The persistent one-grid kernel (edge_layer_dyn) runs only where model creation saw 8 XCDs ("xcd_mask" =
+ *     0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD exit, the launch's self-check must raise the
+ *     repair), "edge_layer_repair", "edge_tail_timeout", "edge_tail_norepair" (WRONG results after a
+ *     timeout), "edge_rows_nowait".
  * Returns CHM_E_ARG for an unknown key. */
 int chm_model_set_option(chm_model* m, const char* key, int64_t value);
 

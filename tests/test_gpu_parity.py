@@ -9,8 +9,6 @@ Tolerances (north star: 1e-4 relative fp32, atom types bit-exact):
 * lattices: rtol 1e-4 (absolute floor 1e-4 x max |lattice|).
 """
 
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -920,47 +918,5 @@ def test_edge_pairs_grid_is_bit_identical(cn, nat):
     assert events[1]["layer_repairs"] == 0
     assert events[2]["layer_repairs"] == 12  # 2 decoder pairs x 6 layers
     for k, name in ((1, "static grid"), (2, "static grid + forced repair")):
-        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
-            assert torch.equal(u, v), f"{what}: {name} differs from the two-launch pair schedule"
-
-
-@pytest.mark.skipif(os.environ.get("CHM_TEST_PAIRS_LAYER") != "1",
-                    reason="experimental k_edge16_pairs_layer (option edge_pairs_layer = 2): its first GPU run "
-                           "faulted; set CHM_TEST_PAIRS_LAYER=1 to run it")
-@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [40] * 512])
-def test_edge_pairs_one_grid_is_bit_identical(cn, nat):
-    """Both edge layers in one persistent grid with edge layer 1 on pairs (k_edge16_pairs_layer, option
-    edge_pairs_layer, experimental): every XCD runs a range of layer-2 row tiles and every pair tile they read
-    (neighbouring ranges may compute a shared pair tile twice, identically), each layer-2 job waiting for its
-    pair tiles. One reverse step must equal the two-launch pair schedule bit for bit, also with the repair
-    launches forced ('edge_layer_repair') and with the blocks of one XCD exiting at once ('edge_dyn_skip_xcd':
-    the launch's self-check must raise the repair); the device counters record exactly those repairs."""
-    B, N = len(nat), sum(nat)
-    g = torch.Generator().manual_seed(17)
-    a0 = torch.randint(0, 100, (N,), generator=g)
-    x0 = torch.rand(N, 3, generator=g)
-    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
-    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
-          torch.randn(N, 3, generator=g))
-    model = _model(1000)
-    model.decoder.set_option("edge_pairs", 1)
-    model.decoder.set_option("edge_pairs_layer", 2)
-    model.decoder.set_option("edge_layer_min", 1)  # (the one-grid form for every shape here)
-    outs, events = [], []
-    for layer, repair, skip in ((0, 0, -1), (1, 0, -1), (1, 1, -1), (1, 0, 3)):
-        model.decoder.set_option("edge_layer", layer)
-        model.decoder.set_option("edge_layer_repair", repair)
-        model.decoder.set_option("edge_dyn_skip_xcd", skip)
-        _lib.prof_events(reset=True)
-        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
-        torch.cuda.synchronize()
-        events.append(_lib.prof_events())
-    del model
-    torch.cuda.empty_cache()
-    print("events (two launches, one grid, forced repair, XCD 3 missing):", events)
-    assert events[1]["layer_wait_timeouts"] == 0 and events[1]["layer_repairs"] == 0
-    assert events[2]["layer_repairs"] == 12  # 2 decoder pairs x 6 layers
-    assert events[3]["layer_incomplete"] == 12 and events[3]["layer_repairs"] == 12
-    for k, name in ((1, "one grid"), (2, "one grid + forced repair"), (3, "one grid, an XCD missing + repair")):
         for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
             assert torch.equal(u, v), f"{what}: {name} differs from the two-launch pair schedule"

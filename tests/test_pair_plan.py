@@ -1,7 +1,7 @@
-"""The schedule of both edge layers in one persistent grid on pairs (k_edge16_pairs_layer, edge16.hip pair_plan),
-checked on the CPU through chm_debug_pair_plan: every layer-2 row tile runs exactly once, on one XCD; every S row
-it reads comes from a pair tile inside its XCD's pair range and its [lo, hi] range; every pair tile it reads is
-listed earlier in the same XCD's job list (so its wait is for work already taken: no deadlock); every index the
+"""The schedule of both edge layers in one grid on pairs (k_edge16_pairs_grid, edge16.hip pair_plan),
+checked on the CPU through chm_debug_pair_plan: every layer-2 row tile runs exactly once, in one list; every S row
+it reads comes from a pair tile inside its list's pair range and its [lo, hi] range; every pair tile it reads is
+listed earlier in the same list (so its wait is for work already taken: no deadlock); every index the
 kernel derives (pair flags, job entries) stays inside its buffer."""
 
 import ctypes
