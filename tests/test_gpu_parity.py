@@ -801,6 +801,31 @@ def test_graph_replay_matches_eager(model100, cn, lanes):
             assert torch.equal(se[k], sg[k]), f"t={se[0]} state {k}"
 
 
+def test_pair_grid_graph_replay_matches_eager(cn):
+    """The static pair grid (the default from 256 row tiles) inside captured step graphs: replays give the
+    eager states bit for bit, and no layer-2 job finds its pair tiles written on another XCD, times out or is
+    repaired. (The grid's block -> XCD rotation is not anchored at XCD 0 under graph replay: an absolute XCD
+    check flagged every job there while the eager tests saw none; the check is relative since.)"""
+    model = _model(100)
+    nat = [40] * 64  # 400 row tiles
+    runs, events = [], []
+    for graph in (False, True):
+        _lib.prof_events(reset=True)
+        runs.append(list(model.sample_states(nat, None, 2.0, 1e-5, noise="philox", seed=13, text_embeds=cn[0],
+                                             null_text_embeds=cn[1], clone=True, graph=graph, t_stop=96)))
+        torch.cuda.synchronize()
+        events.append(_lib.prof_events())
+    del model
+    torch.cuda.empty_cache()
+    print("events (eager, graph):", events)
+    for ev in events:
+        assert ev["layer_other_xcd"] == 0 and ev["layer_wait_timeouts"] == 0 and ev["layer_repairs"] == 0
+    assert [s[0] for s in runs[0]] == [s[0] for s in runs[1]]
+    for se, sg in zip(*runs):
+        for k in (1, 2, 3):
+            assert torch.equal(se[k], sg[k]), f"t={se[0]} state {k}"
+
+
 def test_torch_noise_graph_matches_eager(model100, cn):
     """Parity mode (noise='torch', the reference's CPU RNG stream) under the captured step: every
     step's draws go through pinned host buffers into fixed device buffers before the replay. The
