@@ -284,3 +284,4 @@ hipError_t d3pm_sample(int N, int A, int T, const float* logits, long ld_logits,
                        hipStream_t s, int* bad = nullptr);  // bad: see k_d3pm (caller indices checked)
 
 }  // namespace chm
+
