@@ -177,13 +177,12 @@ void edge16_layer_jobs(long R, int P, int D, long* out);         // (host) its b
 hipError_t edge16_init();
 // edge layer 1 on unordered pairs: S rows of both directions of every pair from one GEMM row (edge16.hip)
 hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s);
-// Both edge layers of a CSP layer in one persistent grid with edge layer 1 on pairs (k_edge16_pairs_layer):
-// XCD x runs the row tiles [R x / 8, R (x + 1) / 8) of edge layer 2 and every pair tile they read (the tiles of
-// two neighbouring XCDs' ranges may overlap: both compute them, identically), each from a host-built job list
-// (pair tiles in order, a row tile's 2 P layer-2 jobs placed `lag` pair tiles behind the last pair tile it reads).
-// A layer-2 job waits (bounded) until its XCD has finished every pair tile of its range, so S goes through the
-// XCD's L2. Per batch and layer: cnt [8] job counters, pflag [8][npx] finished column tiles per pair tile, done
-// (finished layer-2 jobs | exited blocks << 32), all zeroed per decoder call.
+// Both edge layers of a CSP layer in one static grid with edge layer 1 on pairs (k_edge16_pairs_grid): list x
+// holds the row tiles [R x / 8, R (x + 1) / 8) of edge layer 2 and every pair tile they read (the tiles of two
+// neighbouring lists' ranges may overlap: both compute them, identically), in the order of a host-built job list
+// (pair tiles in order, a row tile's 2 P layer-2 jobs placed `lag` pair tiles behind the last pair tile it reads);
+// its blocks share one XCD. A layer-2 job waits (bounded) until its list has finished every pair tile of its
+// range, so S goes through that XCD's L2. Per batch and layer: pflag [8][npx], zeroed per decoder call.
 struct PairSched {
   const int2* jobs;    // [8][jstride] {kind, tile index}: kind 1 = pair (pair tile * 2 + column tile), 2 = layer 2
                        // ((row tile * P + conditioning) * 2 + column tile)
@@ -198,7 +197,7 @@ struct PairSched {
 // k_edge16_pairs_grid: static grid of 8 x jstride blocks, block 8 k + x = job k of list x, then the repair launches
 hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int repair_grid,
                                    hipStream_t s);
-// (host) XCD job lists of k_edge16_pairs_layer for an fc batch: row tiles' pair-tile ranges, per XCD its first
+// (host) the job lists of k_edge16_pairs_grid for an fc batch: row tiles' pair-tile ranges, per list its first
 // pair tile and job list (lag in pair tiles)
 struct PairPlan {
   std::vector<int2> rng;

@@ -113,8 +113,8 @@ struct chm_batch {
   int *pi = nullptr, *pj = nullptr;
   int2* pe = nullptr;
   long Ep = 0;
-  // fc, split16: the job lists of both edge layers in one persistent grid on pairs (k_edge16_pairs_layer),
-  // built for P = max_pairs and the model's edge_lag at creation; per layer 16 + 8 npx scheduling words
+  // fc, split16: the job lists of both edge layers in one static grid on pairs (k_edge16_pairs_grid), built for
+  // P = max_pairs and the model's edge_lag at creation; per layer 8 npx pair-tile flags (psched)
   PairPlan pplan;
   int2 *pjobs = nullptr, *prng = nullptr;
   int *pnjobs = nullptr, *ppa = nullptr;

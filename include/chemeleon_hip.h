@@ -347,10 +347,11 @@ int64_t chm_debug_layer_jobs(int64_t R, int P, int lag, int64_t* out, int64_t ca
  * column tile (layer 1) or conditioning * 2 + column tile (layer 2), for k < n. */
 int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out);
 
-/* Host-only test hook: the schedule of both edge layers in one persistent grid on pairs (k_edge16_pairs_layer)
- * for an fc batch of these crystals, P conditionings and lag `lag` (pair tiles). Returns the per-XCD job-list
- * stride J (or a negative CHM_E_*); when the buffers are large enough: rng [2 R] = per layer-2 row tile the pair
- * tiles [lo, hi] it reads, pa / pb [8] = XCD x's pair tiles [pa, pb), njobs [8], jobs [8][J][2] = {kind
+/* Host-only test hook: the schedule of both edge layers in one static grid on pairs (k_edge16_pairs_grid; block
+ * 8 k + x runs job k of list x) for an fc batch of these crystals, P conditionings and lag `lag` (pair tiles).
+ * Returns the job-list stride J (or a negative CHM_E_*); when the buffers are large enough: rng [2 R] = per
+ * layer-2 row tile the pair tiles [lo, hi] it reads, pa / pb [8] = list x's pair tiles [pa, pb), njobs [8],
+ * jobs [8][J][2] = {kind
  * (1 pair, 2 layer 2), tile index (pair tile * 2 + column tile; (row tile * P + conditioning) * 2 + column
  * tile)}. */
 int64_t chm_debug_pair_plan(const int32_t* h_natoms, int B, int P, int lag, int32_t* rng, int64_t cap_rng, int32_t* pa,
