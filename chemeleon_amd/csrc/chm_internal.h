@@ -184,15 +184,15 @@ hipError_t edge_gemm16_pairs(const EdgeArgs& g, hipStream_t s);
 // its blocks share one XCD. A layer-2 job waits (bounded) until its list has finished every pair tile of its
 // range, so S goes through that XCD's L2. Per batch and layer: pflag [8][npx], zeroed per decoder call.
 struct PairSched {
-  const int2* jobs;    // [8][jstride] {kind, tile index}: kind 1 = pair (pair tile * 2 + column tile), 2 = layer 2
-                       // ((row tile * P + conditioning) * 2 + column tile)
-  const int* njobs;    // [8]
+  // [8][jstride] one record per block, all it needs in one load (padding: kind 0): {kind, tile, a, b}. kind 1 = pair
+  // (tile = pair tile * 2 + column tile, a = its flag index in the list), 2 = layer 2 (tile = (row tile * P +
+  // conditioning) * 2 + column tile, [a, b] = the flag indices of the pair tiles it reads)
+  const int4* jobs;
   int jstride;
-  const int2* rng;     // [R] the pair tiles [lo, hi] row tile t reads
-  const int* pa;       // [8] list x's first pair tile
   int npx;             // pflag entries per list
   unsigned* pflag;     // [8][npx]: finished column tiles | their XCD + 1 << (8 + 4 col)
   long R;
+  unsigned long long* trace = nullptr;  // (profiling, CHM_EDGE_TRACE_LAYER=4: per block {hw id, t0, t_wait, t_end, kind, tile})
 };
 // k_edge16_pairs_grid: static grid of 8 x jstride blocks, block 8 k + x = job k of list x, then the repair launches
 hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int repair_grid,
@@ -202,10 +202,12 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
 struct PairPlan {
   std::vector<int2> rng;
   std::vector<int> pa, pb, njobs;
-  std::vector<int2> jobs;  // [8][jstride]
+  std::vector<int2> jobs;   // [8][jstride] {kind, tile}
+  std::vector<int4> djobs;  // [8][jstride] the device records (PairSched::jobs)
   int jstride = 0, npx = 0;
 };
 void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int lag, PairPlan& out);
+bool pair_plan_ok(const PairPlan& pl);  // the device records' flag indices within [0, npx)
 // (split16.hip) W -> row-scaled split rows (perm 0, or 2 = k_edge16's S column order for W2)
 hipError_t split_rows_h(const float* W, int N, int K, void* out, float* wscale, int perm, hipStream_t s,
                         int chunk = 32);

@@ -34,6 +34,12 @@ namespace chm {
 #define CHM_SEG_TABLE 1
 #endif
 constexpr bool kSegTable = CHM_SEG_TABLE;
+// block timelines of the pair grid (CHM_EDGE_TRACE_LAYER=4) are compiled in only by A/B builds
+// (CHM_BUILD_DEFS=-DCHM_GRID_TRACE=1): the product kernel's registers stay as they are
+#ifndef CHM_GRID_TRACE
+#define CHM_GRID_TRACE 0
+#endif
+constexpr bool kGridTrace = CHM_GRID_TRACE;
 
 namespace {
 
@@ -1443,6 +1449,30 @@ void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int 
   }
   out.jobs.assign((size_t)8 * out.jstride, make_int2(0, 0));
   for (int x = 0; x < 8; ++x) std::copy(jl[x].begin(), jl[x].end(), out.jobs.begin() + (size_t)x * out.jstride);
+  // the device records: flag indices relative to the list's first pair tile, so a block loads nothing else
+  out.djobs.assign(out.jobs.size(), make_int4(0, 0, 0, 0));
+  for (int x = 0; x < 8; ++x)
+    for (int k = 0; k < out.njobs[x]; ++k) {
+      const int2 j = out.jobs[(size_t)x * out.jstride + k];
+      int4& d = out.djobs[(size_t)x * out.jstride + k];
+      if (j.x == 1) {
+        d = make_int4(1, j.y, j.y / 2 - out.pa[x], 0);
+      } else {
+        const int2 r = out.rng[j.y / (2 * P)];
+        d = make_int4(2, j.y, r.x - out.pa[x], r.y - out.pa[x]);
+      }
+    }
+}
+
+// every device record's flag indices inside its list's flag words (checked on the host before any upload)
+bool pair_plan_ok(const PairPlan& pl) {
+  if (pl.djobs.size() != (size_t)8 * pl.jstride || pl.npx < 1) return false;
+  for (const int4& d : pl.djobs) {
+    if (d.x == 1 && (d.z < 0 || d.z >= pl.npx)) return false;
+    if (d.x == 2 && (d.z < 0 || d.z > d.w || d.w >= pl.npx)) return false;
+    if (d.x < 0 || d.x > 2) return false;
+  }
+  return true;
 }
 
 // The static-grid form (option edge_pairs_layer = 1): block 8 k + x runs job k of list x (pair_plan), one
@@ -1454,39 +1484,60 @@ void pair_plan(const std::vector<int>& nat, long E, long Ep, long R, int P, int 
 // another L2) or times out raises the layer's repair request (the repair launches recompute the layer).
 __global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeArgs g2, PairSched ps) {
   const int xs = (int)(blockIdx.x & 7u), k = (int)(blockIdx.x >> 3);
-  if (k >= ps.njobs[xs]) return;
-  const int2 j = ps.jobs[(long)xs * ps.jstride + k];
+  const int4 j = ps.jobs[(long)xs * ps.jstride + k];  // (past the end of list xs: kind 0)
   const unsigned me = xcc_id();
+  unsigned* pf = ps.pflag + (long)xs * ps.npx;
+  const unsigned long long t0 = kGridTrace && ps.trace ? rtime() : 0;  // (profiling: block timelines)
+  unsigned long long tw = t0;
+  auto trace_end = [&]() __attribute__((always_inline)) {
+    if (kGridTrace && ps.trace && threadIdx.x == 0) {
+      unsigned long long* o = ps.trace + 6 * (long)blockIdx.x;
+      o[0] = hwid(); o[1] = t0; o[2] = tw; o[3] = rtime(); o[4] = (unsigned)j.x; o[5] = (unsigned)j.y;
+    }
+  };
   if (j.x == 1) {
     pair_tile(g1, j.y, threadIdx.x);
     // every store of this tile has reached the XCD's L2; count the column tile (and a misplaced block)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-      __hip_atomic_fetch_add(ps.pflag + (long)xs * ps.npx + (j.y / 2 - ps.pa[xs]),
-                             1u + ((me + 1u) << (8 + 4 * (j.y & 1))), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(pf + j.z, 1u + ((me + 1u) << (8 + 4 * (j.y & 1))), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    trace_end();
     return;
   }
   if (j.x != 2) return;
-  if (threadIdx.x == 0) {  // wait (bounded) until both column tiles of every pair tile read are in
-    const int2 r = ps.rng[j.y / (2 * g2.npairs)];
+  if (threadIdx.x < 64) {
+    // wait (bounded) until both column tiles of every pair tile read are in: lane l polls flag j.z + l (64 at a
+    // time), so the pair tiles' flags cost one load latency together instead of one each
+    const int lane = (int)threadIdx.x;
     bool late = false, other = false;
-    for (int p = r.x; p <= r.y && !late; ++p) {
-      const unsigned* f = ps.pflag + (long)xs * ps.npx + (p - ps.pa[xs]);
-      unsigned v, spins = 0;
-      while (((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffu) < 2u &&
-             ++spins < (1u << 21))
+    for (int p0 = j.z; p0 <= j.w && !late; p0 += 64) {
+      const int p = p0 + lane;
+      const bool mine = p <= j.w;
+      unsigned v = mine ? __hip_atomic_load(pf + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 2u;
+      unsigned spins = 0;
+      while (__any((v & 0xffu) < 2u) && ++spins < (1u << 21)) {
         __builtin_amdgcn_s_sleep(4);
-      late = (v & 0xffu) < 2u;
-      other |= ((v >> 8) & 15u) != me + 1u || ((v >> 12) & 15u) != me + 1u;
+        if ((v & 0xffu) < 2u) v = __hip_atomic_load(pf + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      late = __any((v & 0xffu) < 2u);
+      other |= __any(mine && (((v >> 8) & 15u) != me + 1u || ((v >> 12) & 15u) != me + 1u));
     }
-    if (late || other || (g2.dbg & 512))  // (dbg 512, tests: option edge_layer_repair)
-      __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (late) count_event(EV_LAYER_TIMEOUT);
-    else if (other) count_event(EV_LAYER_XCD);
+    if (lane == 0) {
+      if (late || other || (g2.dbg & 512))  // (dbg 512, tests: option edge_layer_repair)
+        __hip_atomic_store(g2.xbad, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (late) count_event(EV_LAYER_TIMEOUT);
+      else if (other) count_event(EV_LAYER_XCD);
+      if (kGridTrace && ps.trace) tw = rtime();
+    }
   }
   __syncthreads();
   edge16_tile<EPI_SEGMEAN, true>(g2, 0, 0, j.y);
+  if (kGridTrace && ps.trace) {
+    __syncthreads();
+    trace_end();
+  }
 }
 
 hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const PairSched& ps, int repair_grid,
@@ -1498,8 +1549,7 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
       !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags ||
       (long)g2.ntiles != ps.R || (long)g2.ntiles * BM < g2.E)
     return hipErrorInvalidValue;
-  if (!ps.jobs || !ps.njobs || !ps.rng || !ps.pa || !ps.pflag)
-    return hipErrorInvalidValue;
+  if (!ps.jobs || !ps.pflag || ps.jstride < 1 || ps.npx < 1) return hipErrorInvalidValue;
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
   hipError_t e = hipGetLastError();

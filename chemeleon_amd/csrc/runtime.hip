@@ -96,7 +96,7 @@ struct chm_model {
   int repair_grid = 0;   // CHM_REPAIR_GRID: blocks of the edge kernels' repair launches (default: ncu)
   int film = 1;          // 0: time_dim = text_dim = 0 (no FilmLayer: the CrystalClip graph encoder)
   const char* edge_trace = nullptr;  // CHM_EDGE_TRACE=file: one edge-GEMM launch's block timeline
-  int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2 (two-launch schedule), 3 (k_edge16_layer)
+  int edge_trace_layer = 1;          // CHM_EDGE_TRACE_LAYER: 1 or 2 (two-launch schedule), 3 (k_edge16_layer), 4 (pair grid)
   std::vector<LayerW> layers;
 };
 
@@ -116,8 +116,7 @@ struct chm_batch {
   // fc, split16: the job lists of both edge layers in one static grid on pairs (k_edge16_pairs_grid), built for
   // P = max_pairs and the model's edge_lag at creation; per layer 8 npx pair-tile flags (psched)
   PairPlan pplan;
-  int2 *pjobs = nullptr, *prng = nullptr;
-  int *pnjobs = nullptr, *ppa = nullptr;
+  int4* pjobs = nullptr;  // the pair grid's block records (PairSched::jobs)
   unsigned* psched = nullptr;
   int2* tiles;  // node ranges [x, y) whose edge rows fit one 256-row GEMM tile
   int ntiles;
@@ -754,10 +753,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->pe = (int2*)carve(b->Ep * sizeof(int2));
   }
   if (!b->pplan.jobs.empty()) {  // (and the one-grid pair schedule: job lists, ranges, per-layer words)
-    b->pjobs = (int2*)carve(b->pplan.jobs.size() * sizeof(int2));
-    b->prng = (int2*)carve(b->pplan.rng.size() * sizeof(int2));
-    b->pnjobs = (int*)carve(8 * sizeof(int));
-    b->ppa = (int*)carve(8 * sizeof(int));
+    b->pjobs = (int4*)carve(b->pplan.djobs.size() * sizeof(int4));
     b->psched = (unsigned*)carve((size_t)L * 8 * b->pplan.npx * sizeof(unsigned));
   }
   if (b->nrt > 0) {  // fc: row tiles of edge layer 2, the partial sums of cut nodes, the fallback rows
@@ -844,8 +840,13 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->nrt = t.knn ? 0 : t.nrt;
   b->r2tot = t.knn ? 0 : t.r2tot;
   b->Ep = t.knn ? 0 : t.Ep;
-  if (!t.knn && b->math == MATH_SPLIT16 && t.E > 0)
+  if (!t.knn && b->math == MATH_SPLIT16 && t.E > 0) {
     pair_plan(t.nat, t.E, t.Ep, t.nrt, b->P, m->edge_lag, b->pplan);
+    if (!pair_plan_ok(b->pplan)) {
+      delete b;
+      return fail(CHM_E_UNSUPPORTED, "pair grid plan: a flag index outside its list");
+    }
+  }
   const size_t need = batch_layout(b, m, nullptr, b->ntiles);
   char* base = (char*)d_ws;
   if (!base) {
@@ -901,10 +902,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->pj, t.pj.data(), t.pj.size() * sizeof(int));
     up(b->pe, t.pe.data(), t.pe.size() * sizeof(int2));
     if (b->pjobs) {
-      up(b->pjobs, b->pplan.jobs.data(), b->pplan.jobs.size() * sizeof(int2));
-      up(b->prng, b->pplan.rng.data(), b->pplan.rng.size() * sizeof(int2));
-      up(b->pnjobs, b->pplan.njobs.data(), 8 * sizeof(int));
-      up(b->ppa, b->pplan.pa.data(), 8 * sizeof(int));
+      up(b->pjobs, b->pplan.djobs.data(), b->pplan.djobs.size() * sizeof(int4));
     }
     if (e == hipSuccess && b->rcnt)  // (the counters return to 0 at the end of every launch)
       e = hipMemsetAsync(b->rcnt, 0, (size_t)b->P * b->nrt * 8 * sizeof(unsigned), s);
@@ -1035,6 +1033,7 @@ extern "C" int64_t chm_debug_pair_plan(const int32_t* h_natoms, int B, int P, in
   const long R = (t.E + kTileRows - 1) / kTileRows;
   PairPlan pl;
   pair_plan(t.nat, t.E, t.Ep, R, P, lag, pl);
+  if (!pair_plan_ok(pl)) return fail(CHM_E_UNSUPPORTED, "pair grid plan: a flag index outside its list");
   if (rng && cap_rng >= 2 * R)
     for (long k = 0; k < R; ++k) { rng[2 * k] = pl.rng[k].x; rng[2 * k + 1] = pl.rng[k].y; }
   for (int x = 0; x < 8; ++x) {
@@ -1163,7 +1162,7 @@ static hipError_t run_edge_gemm(const chm_batch* b, GemmArgs g, int epi, const v
   return gemm_bf16x3_big(g, epi, s);
 }
 
-// profiling (CHM_EDGE_TRACE=file, CHM_EDGE_TRACE_LAYER=1|2): the 4th eager launch of edge layer
+// profiling (CHM_EDGE_TRACE=file, CHM_EDGE_TRACE_LAYER=1-4): the 4th eager launch of edge layer
 // 1 or 2 records {hw id, t0, t_mainloop, t_end, ...} per block (s_memrealtime), dumped to the file
 template <class F>
 static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which, long E, hipStream_t s, F&& launch) {
@@ -1173,7 +1172,8 @@ static hipError_t traced_edge_launch(const chm_model* m, EdgeArgs& ea, int which
                   hipStreamIsCapturing(s, &cst) == hipSuccess && cst == hipStreamCaptureStatusNone && ++traced == 4;
   if (!tr) return launch();
   unsigned long long* tbuf = nullptr;
-  const long tblocks = (which == 3 ? 48 * (E / 256 + 1) : 4 * (E / 128 + 1)) + 4096;  // (3: slot 8 k + XCD)
+  // (3: slot 8 k + XCD; 4, the pair grid: 8 x its longest job list, at most E / 32 jobs)
+  const long tblocks = (which == 4 ? E / 4 : which == 3 ? 48 * (E / 256 + 1) : 4 * (E / 128 + 1)) + 4096;
   hipError_t e = hipMalloc(&tbuf, tblocks * 48);
   if (e == hipSuccess) e = hipMemsetAsync(tbuf, 0, tblocks * 48, s);
   if (e != hipSuccess) return e;
@@ -1364,10 +1364,17 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
         e1p.xbad = e2.xbad = b->xbad + l;
         PairSched ps;
-        ps.jobs = b->pjobs; ps.njobs = b->pnjobs; ps.jstride = b->pplan.jstride; ps.rng = b->prng; ps.pa = b->ppa;
+        ps.jobs = b->pjobs; ps.jstride = b->pplan.jstride;
         ps.npx = b->pplan.npx; ps.pflag = b->psched + (size_t)l * 8 * b->pplan.npx; ps.R = b->nrt;
         ProfScope ps_(CHM_K_EDGE_LAYER, s);
-        HIPCHK(edge_gemm16_pairs_layer(e1p, e2, ps, m->repair_grid, s));
+        // (CHM_EDGE_TRACE_LAYER=4: block timelines of this grid, slot = blockIdx)
+        HIPCHK(traced_edge_launch(m, e2, 4, E, s, [&] {
+          ps.trace = e2.trace;
+          e2.trace = nullptr;
+          const hipError_t r = edge_gemm16_pairs_layer(e1p, e2, ps, m->repair_grid, s);
+          ps.trace = nullptr;
+          return r;
+        }));
       } else if (pairs) {
         // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
         EdgeArgs e1p = e1;
