@@ -1374,6 +1374,20 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
   }
 }
 
+// the pair grid's first repair launch (exits at once unless the grid raised its repair request): clear layer
+// 2's agg row maxima and row-tile counters, then recompute every pair tile (grid-stride); the layer-2 repair
+// launch behind it recomputes edge layer 2
+__global__ __launch_bounds__(512, 1) void k_edge16_pairs_repair(EdgeArgs g, long ntiles, unsigned* agg_max, long nmax,
+                                                                unsigned* rcnt, long nrcnt) {
+  if (__hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nmax; k += (long)gridDim.x * 512) agg_max[k] = 0u;
+  for (long k = (long)blockIdx.x * 512 + threadIdx.x; k < nrcnt; k += (long)gridDim.x * 512) rcnt[k] = 0u;
+  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    pair_tile(g, t, threadIdx.x);
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
   // (repair launches, g.xbad set: run only when the one-grid launch before raised its repair request)
   if (g.xbad && __hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
@@ -1554,15 +1568,14 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
   hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (g1.dbg & 16384)) return e;  // (dbg 16384: profiling / tests, no repair launches)
-  // the repair launches (exit at once unless a wait timed out or layer-2 jobs are missing): clear layer 2's
-  // agg row maxima and row-tile counters, recompute every pair tile, then every layer-2 tile (two launches)
+  // the repair launches (exit at once unless a wait timed out or saw another XCD): clear layer 2's agg row
+  // maxima and row-tile counters and recompute every pair tile, then every layer-2 tile (two launches; r5: the
+  // clearing and the pair tiles were two launches, 4.5 us more per layer when nothing is repaired)
   const unsigned rg = (unsigned)(repair_grid > 0 ? repair_grid : 256);
   EdgeArgs r1 = g1, r2 = g2;
-  hipLaunchKernelGGL((k_edge16_repair<EPI_EDGE, false>), dim3(rg), dim3(512), LDS_B, s, r1, 0L, g2.agg_max,
-                     g2.agg_max ? (long)g2.npairs * g2.nnodes : 0L, (unsigned*)nullptr, 0L, -1, g2.rcnt,
-                     (long)g2.npairs * g2.ntiles * 8);
   const long nb1 = (g1.Mp + PBM - 1) / PBM * (H / BN);
-  hipLaunchKernelGGL(k_edge16_pairs, dim3((unsigned)nb1), dim3(512), LDS_B, s, r1);
+  hipLaunchKernelGGL(k_edge16_pairs_repair, dim3(rg), dim3(512), LDS_B, s, r1, nb1, g2.agg_max,
+                     g2.agg_max ? (long)g2.npairs * g2.nnodes : 0L, g2.rcnt, g2.rcnt ? (long)g2.npairs * g2.ntiles * 8 : 0L);
   const long nb2 = (long)g2.ntiles * g2.npairs * (g2.N / BN);
   hipLaunchKernelGGL((k_edge16_repair<EPI_SEGMEAN, true>), dim3(rg), dim3(512), LDS_B, s, r2, nb2, (unsigned*)nullptr,
                      0L, (unsigned*)nullptr, 0L, (int)EV_LAYER_REPAIR);
@@ -1574,7 +1587,7 @@ static hipError_t edge16_init_once() {
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
-                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_grid};
+                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_grid, (const void*)k_edge16_pairs_repair};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
