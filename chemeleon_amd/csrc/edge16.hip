@@ -1116,7 +1116,10 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
   constexpr int rowB = FD * 4;       // one split row of K = 768
   // glds: wave w stages A rows 16 w .. 16 w + 15 (2 instructions) and W rows 32 w .. 32 w + 31 (4); lane ->
   // row base + 8 q + (lane >> 3), LDS chunk lane & 7 holding line chunk (lane & 7) ^ ((row >> 1) & 7)
-  const char* Ablk = reinterpret_cast<const char*>(g.A) + row0 * rowB;
+  // (traced A/B builds only, dbg 32768: the pair tiles read their F rows from the first 16 pair tiles, which stay
+  // L2-resident: the tile time without F's HBM reads; wrong results)
+  const long arow0 = (kGridTrace && (g.dbg & 32768)) ? row0 % (16 * PBM) : row0;
+  const char* Ablk = reinterpret_cast<const char*>(g.A) + arow0 * rowB;
   const char* Wblk = reinterpret_cast<const char*>(g.W) + (long)n0 * rowB;
   const int ra0 = wave * 16 + (lane >> 3), rw0 = wave * 32 + (lane >> 3);
   const unsigned aoff = (unsigned)(ra0 * rowB) + 16u * (unsigned)((lane & 7) ^ ((ra0 >> 1) & 7));

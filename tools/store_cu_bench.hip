@@ -1,6 +1,9 @@
 // Per-CU store rate against the number of CUs storing at once: `nb` blocks (one per CU: 160 KB of
 // LDS each), every block writes `reps` x 256 KB with edge layer 1's S pattern ("rows": 32 B of a
 // 128-B line per lane pair) or whole lines, into its own region of a 3.36 GB buffer.
+// Round 5 adds the pair epilogue's pattern ("dpp": each instruction writes 8 rows' whole 128-B lines, a line's
+// 8 lanes being l16 in {2m, 2m+1} x g4 = 0..3, so every quarter-wave of 16 lanes holds 32 B of 8 lines) and
+// "quad" (8 rows' whole lines again, a line's 8 lanes consecutive: a quarter-wave holds 2 whole lines).
 //   hipcc --offload-arch=gfx950 -O3 tools/store_cu_bench.hip -o tools/store_cu_bench && tools/store_cu_bench
 #include <hip/hip_runtime.h>
 
@@ -17,7 +20,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
     }                                                          \
   } while (0)
 
-template <bool ROWS>
+template <int PAT>  // 1 rows, 0 lines, 2 dpp, 3 quad
 __global__ __launch_bounds__(512) void k_store(char* __restrict__ out, long tiles_per_block, int reps) {
   extern __shared__ char lds[];  // (only to hold one block per CU)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -29,7 +32,14 @@ __global__ __launch_bounds__(512) void k_store(char* __restrict__ out, long tile
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       long off;
-      if (ROWS) {
+      if (PAT == 2) {  // k: 16 row groups of 8 rows x 2 (the st_e / st_o stores), 4 chunks cycled
+        const int l16 = lane & 15, g4 = lane >> 4, odd = l16 & 1;
+        const int row = wave * 32 + (k >> 2) % 4 * 8 + (l16 >> 1), cc = k & 3;
+        off = (long)row * 2048 + cc * 128 + g4 * 16 + odd * 64;
+      } else if (PAT == 3) {
+        const int row = wave * 32 + (k >> 2) % 4 * 8 + (lane >> 3), cc = k & 3;
+        off = (long)row * 2048 + cc * 128 + (lane & 7) * 16;
+      } else if (PAT == 1) {
         const int i = k >> 4, j = (k >> 2) & 3, sidx = k & 3;
         const int row = (wave & 3) * 64 + i * 32 + r32;
         const int inl = (sidx & 1) * 16 + (sidx >> 1) * 64 + h * 32;
@@ -47,21 +57,25 @@ int main() {
   const long big = 3360L << 20;
   char* buf;
   CK(hipMalloc(&buf, big));
-  CK(hipFuncSetAttribute((const void*)k_store<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  CK(hipFuncSetAttribute((const void*)k_store<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (const void* k : {(const void*)k_store<0>, (const void*)k_store<1>, (const void*)k_store<2>, (const void*)k_store<3>})
+    CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int reps = 48;  // 12 MB per block
   for (int pass = 0; pass < 2; ++pass)
-    for (int rows = 1; rows >= 0; --rows)
+    for (int rows : {1, 0, 2, 3})
       for (int nb : {8, 32, 64, 128, 192, 256}) {
         const long tpb = big / (256L * 1024) / 256;  // each block's region: 51 tiles of 256 KB
         auto launch = [&] {
-          if (rows)
-            hipLaunchKernelGGL(k_store<true>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
+          if (rows == 1)
+            hipLaunchKernelGGL(k_store<1>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
+          else if (rows == 0)
+            hipLaunchKernelGGL(k_store<0>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
+          else if (rows == 2)
+            hipLaunchKernelGGL(k_store<2>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
           else
-            hipLaunchKernelGGL(k_store<false>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
+            hipLaunchKernelGGL(k_store<3>, dim3(nb), dim3(512), 160 * 1024, 0, buf, tpb, reps);
         };
         launch();
         CK(hipDeviceSynchronize());
@@ -74,7 +88,7 @@ int main() {
         ms /= 3;
         const double bytes = (double)nb * reps * 256 * 1024;
         if (pass == 1)
-          printf("%-5s pattern, %3d CUs storing: %.3f ms, %.2f TB/s total, %.1f GB/s per CU\n", rows ? "rows" : "lines", nb,
+          printf("%-5s pattern, %3d CUs storing: %.3f ms, %.2f TB/s total, %.1f GB/s per CU\n", rows == 1 ? "rows" : rows == 0 ? "lines" : rows == 2 ? "dpp" : "quad", nb,
                  ms, bytes / (ms * 1e-3) / 1e12, bytes / nb / (ms * 1e-3) / 1e9);
       }
   return 0;
