@@ -226,7 +226,7 @@ hipError_t node_gemm(const GemmArgs& g, hipStream_t s);
 hipError_t node_gemm_init();
 extern int g_node_variant;  // microbenchmark probes of node_gemm (0 in the product)
 extern int g_node_blocks;   // S16 node GEMM blocks per CU override (microbenchmarks; 0 = default)
-extern int g_node_rows;     // S16 node GEMM tile rows override (microbenchmarks; 0 = default, 64, 128)
+extern int g_node_rows;     // node GEMM tile rows override (microbenchmarks; 0 = default, 64, 128)
 extern int g_node_cols;     // S16 64-row node GEMM tile columns override (microbenchmarks; 0 = default, 64, 128)
 // 256x256 tile, fp16 hi/lo split (three products) for operands with |A| <= 1 (Fourier features)
 hipError_t split_planes(const float* src, long n, void* dst, hipStream_t s);

@@ -50,11 +50,12 @@ template <bool S16, int NMT = 128> constexpr int STB = S16 ? A_STB<NMT> + 2 * W_
 // NB = blocks per CU. 128-row tiles: 2 (bf16x3: 4 stages; S16: 5) or, S16 only, 3 (3 stages of
 // 16 KB); 64-row tiles (S16): 3 (4 stages of 12 KB) or 4 (3 stages)
 template <bool S16, int NB, int NMT = 128>
-constexpr int NST = NMT == 64 ? (NB == 3 ? 4 : 3) : NB == 3 ? 3 : (S16 ? 5 : 4);
+constexpr int NST = NMT == 64 ? (!S16 ? 5 : NB == 3 ? 4 : 3) : NB == 3 ? 3 : (S16 ? 5 : 4);
 constexpr int NODE_LDS = 80 * 1024;  // two blocks per CU
 static_assert(STB<true> * NST<true, 2> <= NODE_LDS && STB<false> * NST<false, 2> <= NODE_LDS, "LDS");
 static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
 static_assert(3 * STB<true, 64> * NST<true, 3, 64> <= 160 * 1024 && 4 * STB<true, 64> * NST<true, 4, 64> <= 160 * 1024, "LDS");
+static_assert(STB<false, 64> * NST<false, 2, 64> <= NODE_LDS, "LDS");  // bf16x3 64-row tiles, two blocks per CU
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -167,7 +168,7 @@ __device__ __forceinline__ void node_epilogue_split(const GemmArgs& g, f32x16 (&
 // shape, so all tilings are bit-identical.
 template <int VAR, bool S16, int NB, int NMT = 128, bool PS = false, int NNT = 128>
 __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
-  static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : S16 && NMT == 64 && (NB == 3 || NB == 4),
+  static_assert(NMT == 128 ? NB == 2 || (S16 && NB == 3) : NMT == 64 && (S16 ? NB == 3 || NB == 4 : NB == 2),
                 "tiling");
   static_assert(!PS || S16, "pre-split A is a split16 form");
   static_assert(NNT == 128 || (NNT == 64 && S16 && !PS && NMT == 64), "64-column tiles: split16, 64 rows");
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
   constexpr int STB_ = NNT == 128 ? STB<S16, NMT> : A_STB_ + NNT * 64;
   constexpr int NST_ = NNT == 128 ? NST<S16, NB, NMT> : 4, AHEAD = NST_;
   constexpr int NWI = S16 ? NNT / 64 : 3;                                // W glds per thread and K-tile
-  constexpr int GL = S16 ? NWI + NI : 5;                                 // glds per thread and K-tile
+  constexpr int GL = S16 ? NWI + NI : 3 + NI;                            // glds per thread and K-tile
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -483,19 +484,20 @@ int g_node_variant = 0;
 
 constexpr int LDS3 = STB<true> * NST<true, 3>;
 constexpr int LDS64_3 = STB<true, 64> * NST<true, 3, 64>, LDS64_4 = STB<true, 64> * NST<true, 4, 64>;
+constexpr int LDS64_B3 = STB<false, 64> * NST<false, 2, 64>;  // bf16x3 64-row tiles (5 stages of 16 KB)
 
 static hipError_t node_gemm_init_once() {
-  const void* ks[14] = {(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
+  const void* ks[15] = {(const void*)k_node_gemm<0, false, 2, 64>,(const void*)k_node_gemm<0, false, 2>,    (const void*)k_node_gemm<1, false, 2>,
                         (const void*)k_node_gemm<0, true, 2>,     (const void*)k_node_gemm<1, true, 2>,
                         (const void*)k_node_gemm<0, true, 3>,     (const void*)k_node_gemm<1, true, 3>,
                         (const void*)k_node_gemm<0, true, 3, 64>, (const void*)k_node_gemm<1, true, 3, 64>,
                         (const void*)k_node_gemm<0, true, 4, 64>, (const void*)k_node_gemm<1, true, 4, 64>,
                         (const void*)k_node_gemm<0, true, 2, 128, true>, (const void*)k_node_gemm<0, true, 3, 128, true>,
                         (const void*)k_node_gemm<0, true, 3, 64, true>, (const void*)k_node_gemm<0, true, 4, 64, true>};
-  const int bytes[14] = {NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4,
+  const int bytes[15] = {LDS64_B3, NODE_LDS, NODE_LDS, NODE_LDS, NODE_LDS, LDS3, LDS3, LDS64_3, LDS64_3, LDS64_4, LDS64_4,
                          NODE_LDS, LDS3, LDS64_3, LDS64_4};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 14 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
+  for (int i = 0; i < 15 && e == hipSuccess; ++i) e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, bytes[i]);
   return e;
 }
 
@@ -506,7 +508,7 @@ hipError_t node_gemm_init() {
 }
 
 int g_node_blocks = 0;  // S16 blocks per CU override (microbenchmarks): 0 = default
-int g_node_rows = 0;    // S16 tile rows override (microbenchmarks): 0 = default, 64, 128
+int g_node_rows = 0;    // tile rows override (microbenchmarks): 0 = default, 64, 128
 int g_node_cols = 0;    // S16 64-row tile columns override (microbenchmarks): 0 = default, 64, 128
 
 // bf16x3 when g.wscale is null (g.Wp3 = three bf16 planes), S16 otherwise (g.Wp3 = split_rows_h
@@ -561,6 +563,13 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   // S16: three blocks per CU (3 stages each): more waves to hide the K-loop latency (-7% at
   // M = 40960, -17% at M = 20480 against two blocks with 5 stages)
   const int nb = g_node_blocks ? g_node_blocks : 3;
+  if (!g.wscale && rows == 64 && !v1) {
+    // bf16x3 on grids short of one 128-row block per CU (the heads and conditioning GEMMs at the small shapes):
+    // 64-row tiles, half of each wave's MFMAs per K-step on the K loop's dependent chain; bit-identical
+    const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
+    hipLaunchKernelGGL((k_node_gemm<0, false, 2, 64>), grid64, block, LDS64_B3, s, g);
+    return hipGetLastError();
+  }
   if (g.wscale && nb == 3)
     hipLaunchKernelGGL((v1 ? k_node_gemm<1, true, 3> : k_node_gemm<0, true, 3>), grid, block, LDS3, s, g);
   else if (g.wscale)

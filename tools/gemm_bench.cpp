@@ -199,6 +199,26 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "b3rows") {  // bf16x3 node GEMM: 128- vs 64-row tiles (short grids)
+    CK(node_gemm_init());
+    const size_t nc = (size_t)M * N;
+    std::vector<float> c128(nc), c64(nc);
+    for (int rep = 0; rep < 2; ++rep) {
+      g_node_rows = 128;
+      float t128 = time_it(50, s, [&] { CK(node_gemm(g, s)); });
+      CK(node_gemm(g, s)); CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(c128.data(), C, nc * 4, hipMemcpyDeviceToHost));
+      CK(hipMemset(C, 0, nc * 4));
+      g_node_rows = 64;
+      float t64 = time_it(50, s, [&] { CK(node_gemm(g, s)); });
+      CK(node_gemm(g, s)); CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(c64.data(), C, nc * 4, hipMemcpyDeviceToHost));
+      g_node_rows = 0;
+      printf("bf16x3 M=%ld N=%d K=%d: 128-row tiles %.2f us | 64-row tiles %.2f us | bit-identical: %s\n", M, N, K,
+             t128 * 1e3, t64 * 1e3, c128 == c64 ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::string(argv[3]) == "node") {  // node GEMM shapes: glds kernel vs register-staged
     CK(node_gemm_init());
     for (int rep = 0; rep < 2; ++rep) {
