@@ -563,9 +563,10 @@ hipError_t node_gemm(const GemmArgs& g_in, hipStream_t s) {
   // S16: three blocks per CU (3 stages each): more waves to hide the K-loop latency (-7% at
   // M = 40960, -17% at M = 20480 against two blocks with 5 stages)
   const int nb = g_node_blocks ? g_node_blocks : 3;
-  if (!g.wscale && rows == 64 && !v1) {
-    // bf16x3 on grids short of one 128-row block per CU (the heads and conditioning GEMMs at the small shapes):
-    // 64-row tiles, half of each wave's MFMAs per K-step on the K loop's dependent chain; bit-identical
+  if (!g.wscale && !v1 && (g_node_rows ? g_node_rows == 64 : 2 * blocks <= 256)) {
+    // bf16x3 where even the 64-row grid fits the CUs in one round (the heads and conditioning GEMMs at the small
+    // shapes): 64-row tiles, half of each wave's MFMAs per K-step on the K loop's dependent chain; bit-identical.
+    // (heads, K = 512: M = 10240 31.3 -> 22.2 us, but M = 20480 34.8 -> 38.9: profiles/r5/node_b3rows/)
     const dim3 grid64((unsigned)(((g.M + 63) / 64) * (g.N / NN)));
     hipLaunchKernelGGL((k_node_gemm<0, false, 2, 64>), grid64, block, LDS64_B3, s, g);
     return hipGetLastError();
