@@ -2,7 +2,7 @@
 # rocprof kernel stats at 512x40 / 64x40 / 64x20. Repo root, GPU box.
 set -e
 R=${GRAFT_REPO_ROOT:-.}
-O=$R/gpurun_out/final5b
+O=$R/gpurun_out/${FINAL_TAG:-final5b}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.txt 2>&1 || { tail -n 40 $O/gputests.txt; exit 1; }
