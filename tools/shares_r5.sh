@@ -2,7 +2,7 @@
 # inside the timed region): n_samples 512 / N
 set -e
 R=${GRAFT_REPO_ROOT:-.}
-O=$R/gpurun_out/shares5
+O=$R/gpurun_out/${SHARES_TAG:-shares5}
 mkdir -p $O
 for rep in 1 2; do
   for n in 512 256 128 64; do
