@@ -1391,9 +1391,9 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_repair(EdgeArgs g, long
   }
 }
 
+// edge layer 1 on pairs as a launch of its own (the two-launch schedule; the pair grid's repairs use
+// k_edge16_pairs_repair)
 __global__ __launch_bounds__(512, 1) void k_edge16_pairs(EdgeArgs g) {
-  // (repair launches, g.xbad set: run only when the one-grid launch before raised its repair request)
-  if (g.xbad && __hip_atomic_load(g.xbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   pair_tile(g, remap(blockIdx.x, gridDim.x), threadIdx.x);
 }
 
