@@ -199,6 +199,24 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::string(argv[3]) == "s16order") {  // split16 default vs explicit 128-row / 3-block launch, interleaved
+    CK(node_gemm_init());
+    void* W16; float* wsc16; float* amax;
+    CK(hipMalloc(&W16, 2L * N * K * 2)); CK(hipMalloc(&wsc16, N * 4)); CK(hipMalloc(&amax, M * 4));
+    CK(split_rows_h(W, N, K, W16, wsc16, 0, s, 16));
+    std::vector<float> one(M, 1.0f);
+    CK(hipMemcpy(amax, one.data(), M * 4, hipMemcpyHostToDevice));
+    GemmArgs g16 = g; g16.Wp3 = W16; g16.wscale = wsc16; g16.amax = amax;
+    for (int rep = 0; rep < 4; ++rep) {
+      g_node_rows = 0; g_node_blocks = 0;
+      float td = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+      g_node_rows = 128; g_node_blocks = 3;
+      float te = time_it(50, s, [&] { CK(node_gemm(g16, s)); });
+      g_node_rows = 0; g_node_blocks = 0;
+      printf("split16 M=%ld N=%d K=%d: default %.2f us | explicit 128 rows x 3 blocks %.2f us\n", M, N, K, td * 1e3, te * 1e3);
+    }
+    return 0;
+  }
   if (argc > 3 && std::string(argv[3]) == "b3rows") {  // bf16x3 node GEMM: 128- vs 64-row tiles (short grids)
     CK(node_gemm_init());
     const size_t nc = (size_t)M * N;
