@@ -503,8 +503,19 @@ __global__ __launch_bounds__(256) void k_graph_heads(const float* __restrict__ H
 #pragma unroll
   for (int q = 0; q < 9; ++q) part[q] = 0.f;
   for (int col = threadIdx.x; col < H; col += 256) {
+    // the node sum in node order, its loads issued 8 at a time ahead of the adds (one dependent load per node
+    // made this a chain of n load latencies: 13.5 us at n = 20)
     float sacc = 0.f;
-    for (int k = 0; k < n; ++k) sacc += Hf[(r0 + k) * H + col];
+    const float* hc = Hf + r0 * H + col;
+    int k = 0;
+    for (; k + 8 <= n; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = hc[(long)(k + u) * H];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sacc += v[u];
+    }
+    for (; k < n; ++k) sacc += hc[(long)k * H];
     const float mean = sacc / (float)(n < 1 ? 1 : n);
 #pragma unroll
     for (int q = 0; q < 9; ++q) part[q] += Wlat[q * H + col] * mean;
