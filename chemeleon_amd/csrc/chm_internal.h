@@ -235,10 +235,6 @@ extern int g_gemm3_variant;  // tuning switch of gemm_bf16x3 (bench only)
 hipError_t fourier(const float* x, const int* ei, const int* ej, long E, float* F, hipStream_t s);
 hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int* node_off, const long* edge_off,
                         const int* natoms, long N, long E, int P, hipStream_t s);
-// rmax != null: rmax[row] = max |Hout[row, :]|
-// (Hs / He: also the rows split for the pre-split node GEMMs, GemmArgs::aex; film_ln's Hls / Hle likewise)
-hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr,
-                 void* Hs = nullptr, int* He = nullptr);
 // d_t != null: the time-embedding row is temb + (*d_t) * TD, shared by all graphs
 hipError_t build_cond_in(const float* temb, int tstride, const int* d_t, const float* text0, const float* text1,
                          int text_dim, float* cin, int B, int P, hipStream_t s);
@@ -247,6 +243,12 @@ constexpr int kGBLayers = 16;
 struct GraphBiasArgs { const float* Wc[kGBLayers]; const float* b1[kGBLayers]; };
 // out[l] (l < nl, [B][H] each, consecutive) = the per-graph term of edge layer 1 of layer l
 hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldwc, float* out, int B, hipStream_t s);
+// rmax != null: rmax[row] = max |Hout[row, :]|
+// (Hs / He: also the rows split for the pre-split node GEMMs, GemmArgs::aex; film_ln's Hls / Hle likewise)
+// ga != null: the same launch also writes graph_bias(lat, *ga, nl, ldwc, gout, B)'s per-graph terms
+hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr,
+                 void* Hs = nullptr, int* He = nullptr, const float* lat = nullptr, const GraphBiasArgs* ga = nullptr,
+                 int nl = 0, long ldwc = 0, float* gout = nullptr, int B = 0);
 // rmx != null (split16 node GEMMs): rows of the four row-max arrays [4][rstride] (RMX_*): writes
 // max |Hl[row, :]| to RMX_HL and zeroes RMX_H, RMX_AGG, RMX_U for this layer's atomic maxima
 enum { RMX_H = 0, RMX_HL = 1, RMX_AGG = 2, RMX_U = 3 };

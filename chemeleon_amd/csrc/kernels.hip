@@ -316,10 +316,37 @@ hipError_t segment_mean(const float* msg, float* agg, const int* n2g, const int*
 // ---------------------------------------------------------------------------
 // small node / graph kernels
 // ---------------------------------------------------------------------------
-// one wave per row (4 rows per block); rmax != null: the row's max |value| for the split16 node GEMMs
+// per-graph part of edge layer 1 for up to kGBLayers layers: out[l][g][n] = b1_l[n] + sum_ab W1_l[n, ab] (L L^T)_ab
+// (cspnet.py:144-152, the C block of W1); element idx = g * H + n of layer l
+__device__ __forceinline__ void graph_bias_elem(long idx, int l, const float* __restrict__ lat, const GraphBiasArgs& a,
+                                                long ldwc, float* __restrict__ out, int B) {
+  const float* Wc = a.Wc[l];
+  const int gph = (int)(idx / H), n = (int)(idx % H);
+  const float* L = lat + gph * 9;
+  float v = a.b1[l][n];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float ip = L[i * 3 + 0] * L[j * 3 + 0] + L[i * 3 + 1] * L[j * 3 + 1] + L[i * 3 + 2] * L[j * 3 + 2];
+      v += Wc[n * ldwc + i * 3 + j] * ip;
+    }
+  out[(long)l * B * H + idx] = v;
+}
+
+// one wave per row (4 rows per block); rmax != null: the row's max |value| for the split16 node GEMMs.
+// Blocks past the embedding rows (nbe of them) compute the per-graph terms of the first nl layers (nbg blocks
+// each; graph_bias' work, folded into this launch: one launch less per decoder call)
 __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, const float* __restrict__ emb,
                                                float* __restrict__ Hout, long N, int P, float* __restrict__ rmax,
-                                               void* Hs, int* He) {
+                                               void* Hs, int* He, long nbe, const float* __restrict__ lat,
+                                               GraphBiasArgs ga, long ldwc, float* __restrict__ gout, int B, long nbg) {
+  if ((long)blockIdx.x >= nbe) {
+    const long gb = (long)blockIdx.x - nbe;
+    const long idx = (gb % nbg) * 256 + threadIdx.x;
+    if (idx < (long)B * H) graph_bias_elem(idx, (int)(gb / nbg), lat, ga, ldwc, gout, B);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= N * P) return;
@@ -338,9 +365,14 @@ __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, co
   if (Hs) store_split_row512(v0, v1, lane, Hs, He, r);
 }
 hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax, void* Hs,
-                 int* He) {
+                 int* He, const float* lat, const GraphBiasArgs* ga, int nl, long ldwc, float* gout, int B) {
   const long rows = N * P;
-  hipLaunchKernelGGL(k_embed, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a, emb, Hout, N, P, rmax, Hs, He);
+  const long nbe = (rows + 3) / 4;
+  const long nbg = ga ? ((long)B * H + 255) / 256 : 0;
+  if (ga && (nl < 1 || nl > kGBLayers || !lat || !gout || B < 1)) return hipErrorInvalidValue;
+  const GraphBiasArgs none{};
+  hipLaunchKernelGGL(k_embed, dim3((unsigned)(nbe + (ga ? nbg * nl : 0))), dim3(256), 0, s, a, emb, Hout, N, P, rmax, Hs,
+                     He, nbe, lat, ga ? *ga : none, ldwc, gout, B, nbg > 0 ? nbg : 1);
   return hipGetLastError();
 }
 
@@ -371,25 +403,12 @@ hipError_t decrement(int* d_t, hipStream_t s) {
   return hipGetLastError();
 }
 
-// per-graph part of the first edge layer: b1 + W1[:, 2H:2H+9] . vec(L L^T)
-// per-graph part of edge layer 1 for up to kGBLayers layers in one launch (blockIdx.y = layer):
-// out[l][g][n] = b1_l[n] + sum_ab W1_l[n, ab] (L L^T)_ab (cspnet.py:144-152, the C block of W1)
+// the per-graph terms of layers beyond the first kGBLayers (blockIdx.y = layer; the first kGBLayers run inside
+// k_embed's launch)
 __global__ void k_graph_bias(const float* __restrict__ lat, GraphBiasArgs a, long ldwc, float* __restrict__ out, int B) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)B * H) return;
-  const int l = blockIdx.y;
-  const float* Wc = a.Wc[l];
-  const int gph = (int)(idx / H), n = (int)(idx % H);
-  const float* L = lat + gph * 9;
-  float v = a.b1[l][n];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const float ip = L[i * 3 + 0] * L[j * 3 + 0] + L[i * 3 + 1] * L[j * 3 + 1] + L[i * 3 + 2] * L[j * 3 + 2];
-      v += Wc[n * ldwc + i * 3 + j] * ip;
-    }
-  out[(long)l * B * H + idx] = v;
+  graph_bias_elem(idx, blockIdx.y, lat, a, ldwc, out, B);
 }
 hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldwc, float* out, int B, hipStream_t s) {
   if (nl < 1 || nl > kGBLayers) return hipErrorInvalidValue;

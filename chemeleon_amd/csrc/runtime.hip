@@ -1268,7 +1268,15 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     g.bias = m->bc; g.act = 1;
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
-  HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H), ps ? b->Hs : nullptr, ps ? b->He : nullptr));
+  // the embedding rows and the first kGBLayers layers' per-graph terms of edge layer 1 in one launch
+  GraphBiasArgs ga0;
+  const int nl0 = L < kGBLayers ? L : kGBLayers;
+  for (int l = 0; l < nl0; ++l) {
+    ga0.Wc[l] = m->layers[l].Wcl;
+    ga0.b1[l] = m->layers[l].b1;
+  }
+  HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H), ps ? b->Hs : nullptr, ps ? b->He : nullptr, lat,
+               nl0 > 0 ? &ga0 : nullptr, nl0, 9, b->gbias, B));
   // fc edge layer 1 on unordered pairs (option edge_pairs): F holds the pairs' features only
   const bool pairs = b->math == MATH_SPLIT16 && m->edge_pairs && b->pe && !b->knn && E > 0;
   if (pairs)
@@ -1277,7 +1285,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     HIPCHK(fourier_h(x, b->ei, b->ej, E, b->F, s, b->knn ? b->fd : nullptr));  // fp16 hi/lo split rows
   else
     HIPCHK(fourier(x, b->ei, b->ej, E, b->F, s));
-  for (int l0 = 0; l0 < L; l0 += kGBLayers) {  // all layers' per-graph terms, one launch per 16 layers
+  for (int l0 = kGBLayers; l0 < L; l0 += kGBLayers) {  // the per-graph terms of layers past the first 16
     GraphBiasArgs ga;
     const int nl = L - l0 < kGBLayers ? L - l0 : kGBLayers;
     for (int l = 0; l < nl; ++l) {
