@@ -245,10 +245,12 @@ struct GraphBiasArgs { const float* Wc[kGBLayers]; const float* b1[kGBLayers]; }
 hipError_t graph_bias(const float* lat, const GraphBiasArgs& a, int nl, long ldwc, float* out, int B, hipStream_t s);
 // rmax != null: rmax[row] = max |Hout[row, :]|
 // (Hs / He: also the rows split for the pre-split node GEMMs, GemmArgs::aex; film_ln's Hls / Hle likewise)
-// ga != null: the same launch also writes graph_bias(lat, *ga, nl, ldwc, gout, B)'s per-graph terms
+// ga != null: the same launch also writes graph_bias(lat, *ga, nl, ldwc, gout, B)'s per-graph terms, and zeroes
+// z0[0, n0) and z1[0, n1) (the words a decoder call starts from clear)
 hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax = nullptr,
                  void* Hs = nullptr, int* He = nullptr, const float* lat = nullptr, const GraphBiasArgs* ga = nullptr,
-                 int nl = 0, long ldwc = 0, float* gout = nullptr, int B = 0);
+                 int nl = 0, long ldwc = 0, float* gout = nullptr, int B = 0, unsigned* z0 = nullptr, long n0 = 0,
+                 unsigned* z1 = nullptr, long n1 = 0);
 // rmx != null (split16 node GEMMs): rows of the four row-max arrays [4][rstride] (RMX_*): writes
 // max |Hl[row, :]| to RMX_HL and zeroes RMX_H, RMX_AGG, RMX_U for this layer's atomic maxima
 enum { RMX_H = 0, RMX_HL = 1, RMX_AGG = 2, RMX_U = 3 };

@@ -340,7 +340,15 @@ __device__ __forceinline__ void graph_bias_elem(long idx, int l, const float* __
 __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, const float* __restrict__ emb,
                                                float* __restrict__ Hout, long N, int P, float* __restrict__ rmax,
                                                void* Hs, int* He, long nbe, const float* __restrict__ lat,
-                                               GraphBiasArgs ga, long ldwc, float* __restrict__ gout, int B, long nbg) {
+                                               GraphBiasArgs ga, long ldwc, float* __restrict__ gout, int B, long nbg,
+                                               long nbgt, unsigned* __restrict__ z0, long n0, unsigned* __restrict__ z1,
+                                               long n1) {
+  if ((long)blockIdx.x >= nbe + nbgt) {  // the call's cleared words (the pair grid's repair requests and flags)
+    const long idx = ((long)blockIdx.x - nbe - nbgt) * 256 + threadIdx.x;
+    if (idx < n0) z0[idx] = 0u;
+    else if (idx - n0 < n1) z1[idx - n0] = 0u;
+    return;
+  }
   if ((long)blockIdx.x >= nbe) {
     const long gb = (long)blockIdx.x - nbe;
     const long idx = (gb % nbg) * 256 + threadIdx.x;
@@ -365,14 +373,17 @@ __global__ __launch_bounds__(256) void k_embed(const int64_t* __restrict__ a, co
   if (Hs) store_split_row512(v0, v1, lane, Hs, He, r);
 }
 hipError_t embed(const int64_t* a, const float* emb, float* Hout, long N, int P, hipStream_t s, float* rmax, void* Hs,
-                 int* He, const float* lat, const GraphBiasArgs* ga, int nl, long ldwc, float* gout, int B) {
+                 int* He, const float* lat, const GraphBiasArgs* ga, int nl, long ldwc, float* gout, int B, unsigned* z0,
+                 long n0, unsigned* z1, long n1) {
   const long rows = N * P;
   const long nbe = (rows + 3) / 4;
-  const long nbg = ga ? ((long)B * H + 255) / 256 : 0;
+  const long nbg = ga ? ((long)B * H + 255) / 256 : 0, nbgt = ga ? nbg * nl : 0;
   if (ga && (nl < 1 || nl > kGBLayers || !lat || !gout || B < 1)) return hipErrorInvalidValue;
+  if (n0 < 0 || n1 < 0 || (n0 && !z0) || (n1 && !z1)) return hipErrorInvalidValue;
+  const long nbz = (n0 + n1 + 255) / 256;
   const GraphBiasArgs none{};
-  hipLaunchKernelGGL(k_embed, dim3((unsigned)(nbe + (ga ? nbg * nl : 0))), dim3(256), 0, s, a, emb, Hout, N, P, rmax, Hs,
-                     He, nbe, lat, ga ? *ga : none, ldwc, gout, B, nbg > 0 ? nbg : 1);
+  hipLaunchKernelGGL(k_embed, dim3((unsigned)(nbe + nbgt + nbz)), dim3(256), 0, s, a, emb, Hout, N, P, rmax, Hs, He, nbe,
+                     lat, ga ? *ga : none, ldwc, gout, B, nbg > 0 ? nbg : 1, nbgt, z0, n0, z1, n1);
   return hipGetLastError();
 }
 

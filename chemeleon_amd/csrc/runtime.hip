@@ -1268,6 +1268,17 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     g.bias = m->bc; g.act = 1;
     HIPCHK(run_gemm(b, g, EPI_STD, m->Wc3, s));
   }
+  // fc edge layer 1 on unordered pairs (option edge_pairs): F holds the pairs' features only
+  const bool pairs = b->math == MATH_SPLIT16 && m->edge_pairs && b->pe && !b->knn && E > 0;
+  // (edge layer 1 on pairs as two launches, the default below 256 row tiles: no intra-grid waits, nothing to clear;
+  // the memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
+  // both edge layers on pairs in one grid (k_edge16_pairs_grid) for this call
+  const bool pair_grid = pairs && m->edge_pairs_layer && m->edge_rows && b->rtiles && m->edge_layer && b->psched &&
+                         P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu;
+  const bool waits = !pairs || pair_grid;
+  // the pair grid's repair requests and per-layer flags start clear in every call: zeroed by the embedding launch
+  // below (two memset nodes less per call)
+  const bool zero_grid = b->xbad && b->math == MATH_SPLIT16 && pair_grid;
   // the embedding rows and the first kGBLayers layers' per-graph terms of edge layer 1 in one launch
   GraphBiasArgs ga0;
   const int nl0 = L < kGBLayers ? L : kGBLayers;
@@ -1276,9 +1287,9 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     ga0.b1[l] = m->layers[l].b1;
   }
   HIPCHK(embed(a, m->emb, b->Hres, N, P, s, rmx(RMX_H), ps ? b->Hs : nullptr, ps ? b->He : nullptr, lat,
-               nl0 > 0 ? &ga0 : nullptr, nl0, 9, b->gbias, B));
-  // fc edge layer 1 on unordered pairs (option edge_pairs): F holds the pairs' features only
-  const bool pairs = b->math == MATH_SPLIT16 && m->edge_pairs && b->pe && !b->knn && E > 0;
+               nl0 > 0 ? &ga0 : nullptr, nl0, 9, b->gbias, B, zero_grid ? b->xbad : nullptr,
+               zero_grid ? 2L * kMaxLayers : 0L, zero_grid ? b->psched : nullptr,
+               zero_grid ? (long)L * 8 * b->pplan.npx : 0L));
   if (pairs)
     HIPCHK(fourier_h(x, b->pi, b->pj, b->Ep, b->F, s, nullptr));  // (the (i, j) edges' features, i <= j)
   else if (b->math == MATH_SPLIT16)
@@ -1294,13 +1305,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     }
     HIPCHK(graph_bias(lat, ga, nl, 9, b->gbias + (size_t)l0 * B * H, B, s));
   }
-  // (edge layer 1 on pairs as two launches, the default: no intra-grid waits, nothing to clear; the three
-  // memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
-  // both edge layers on pairs in one grid (k_edge16_pairs_grid) for this call
-  const bool pair_grid = pairs && m->edge_pairs_layer && m->edge_rows && b->rtiles && m->edge_layer && b->psched &&
-                         P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu;
-  const bool waits = !pairs || pair_grid;
-  if (b->xbad && b->math == MATH_SPLIT16 && waits) {
+  if (b->xbad && b->math == MATH_SPLIT16 && waits && !pair_grid) {
     // k_edge16_layer / k_edge16_tail: repair requests (layer l: xbad[l], tail of layer l: xbad[kMaxLayers + l])
     // and row-tile flags start clear in every call (the flags also return to 0 at the end of every
     // launch; this keeps a timed-out wait from leaking into later calls)
@@ -1308,7 +1313,6 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
     if (!pairs && m->edge_rows && m->edge_layer && m->edge_dyn && b->sched)
       HIPCHK(hipMemsetAsync(b->sched, 0, (size_t)L * (16 + 8 * b->sched_cap) * sizeof(unsigned), s));
     if (!pairs && m->edge_rows && m->edge_layer) HIPCHK(hipMemsetAsync(b->lflags, 0, b->nrt * sizeof(unsigned), s));
-    if (pair_grid) HIPCHK(hipMemsetAsync(b->psched, 0, (size_t)L * 8 * b->pplan.npx * sizeof(unsigned), s));
   }
   for (int l = 0; l < L; ++l) {
     const LayerW& w = m->layers[l];
