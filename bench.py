@@ -645,7 +645,7 @@ def main():
                      "kernel": {"split16": ((f"both edge layers of a CSP layer in one grid, layer 1 on "
                                              f"unordered pairs ({msg_kernel}: D.f once per pair i <= j, both "
                                              "directions' S = SiLU(U +- V + P + Q); S.W2^T + SiLU + fused "
-                                             "scatter_mean; 16x16x32 MFMA), both conditionings, incl. its three repair "
+                                             "scatter_mean; 16x16x32 MFMA), both conditionings, incl. its two repair "
                                              "launches (no-ops unless a check fails)") if edge_pairs_on() else
                                             ("both edge layers of a CSP layer in one grid (k_edge16_layer: D.f + P_i + "
                                              "Q_j + SiLU -> S, S.W2^T + SiLU + fused scatter_mean; 16x16x32 MFMA), "

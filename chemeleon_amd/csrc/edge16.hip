@@ -1320,10 +1320,11 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
         const bool st = ok[i] && !nostore && (dir == 0 || (ni[i] != nj[i] && !(g.dbg & 131072)));
         f32x4 v[8];
         float mx = 0.f;
+        const bool nopq = g.dbg & 524288;  // (profiling: P / Q rows not loaded; wrong results)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const f32x4 pv = *reinterpret_cast<const f32x4*>(prow + 16 * j);
-          const f32x4 qv = *reinterpret_cast<const f32x4*>(qrow + 16 * j);
+          const f32x4 pv = nopq ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(prow + 16 * j);
+          const f32x4 qv = nopq ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(qrow + 16 * j);
           const f32x4 x = dir ? accU[i][j] - accV[i][j] : accU[i][j] + accV[i][j];
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {

@@ -1633,16 +1633,30 @@ extern "C" int chm_d3pm_sample(int N, int A, int T, const float* logits, const i
   if (N == 0) return CHM_OK;
   if (!logits || !xt || !tn || !noise || !q1 || !qm || !out) return fail(CHM_E_ARG, "NULL argument");
   hipStream_t s = (hipStream_t)stream;
-  // the device range check: the first node with t outside [1, T] or x_t outside [0, A) (N = none)
-  int* d_bad = nullptr;
-  HIPCHK(hipMallocAsync((void**)&d_bad, sizeof(int), s));
+  // the device range check: the first node with t outside [1, T] or x_t outside [0, A) (N = none), recorded in
+  // one flag word per (host thread, device), allocated on first use; the kernel writes -1 for such a node
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  thread_local std::vector<int*> flag_words;
+  if ((int)flag_words.size() <= dev) flag_words.resize(dev + 1, nullptr);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(s, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!flag_words[dev]) {
+    if (capturing) return fail(CHM_E_UNSUPPORTED, "chm_d3pm_sample: call it once outside capture on this thread first");
+    HIPCHK(hipMalloc((void**)&flag_words[dev], sizeof(int)));
+  }
+  int* d_bad = flag_words[dev];
   int h_bad = N;
   hipError_t e = hipMemsetAsync(d_bad, 0x7f, sizeof(int), s);  // (0x7f7f7f7f: above any node index)
   if (e == hipSuccess)
     e = d3pm_sample(N, A, T, logits, A, nullptr, 1.f, 0.f, xt, tn, 0, nullptr, noise, q1, qm, out, 0, 0, s, d_bad);
+  // under stream capture (a graph): no host readback; out-of-range nodes are the ones with out = -1
+  if (capturing) {
+    if (e != hipSuccess) return fail(CHM_E_HIP, std::string("chm_d3pm_sample: ") + hipGetErrorString(e));
+    return CHM_OK;
+  }
   if (e == hipSuccess) e = hipMemcpyAsync(&h_bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s);
-  const hipError_t ef = hipFreeAsync(d_bad, s);
-  if (e == hipSuccess) e = ef;
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(CHM_E_HIP, std::string("chm_d3pm_sample: ") + hipGetErrorString(e));
   if (h_bad < N)

@@ -7,6 +7,10 @@
 //     address, so nothing it reads can be freed under it;
 //   * every launch goes on the current HIP stream of the batch's device, under a device guard for that
 //     device; every tensor must live on that device (checked on the host before any launch);
+//   * a Batch is scratch for one stream at a time: an op on another stream than the batch's last one first
+//     makes its stream wait for the last one's work (an event) and records the workspace as used on it
+//     (record_stream), so uses on several streams are ordered and the caching allocator reuses the
+//     workspace only after every stream that used it is done;
 //   * outputs and workspaces come from the PyTorch caching allocator (at::empty);
 //   * shapes, dtypes and devices are checked on the host, the C ABI checks element counts again, and a
 //     failing call raises through TORCH_CHECK with chm_last_error() (RuntimeError in Python).
@@ -16,10 +20,14 @@
 // scatter_mean (chemeleon/utils/scatter.py:88-112) and D3PM.p_logits (chemeleon/utils/diff_utils.py:307-329).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <hip/hip_runtime_api.h>
+
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -88,6 +96,9 @@ struct Batch : torch::CustomClassHolder {
   chm_batch* b = nullptr;
   int64_t N = 0, E = 0, B = 0;
   int P = 0, knn = 0;
+  std::mutex mu;                    // guards last / ev (ops from several host threads)
+  hipStream_t last = nullptr;       // the stream of the last op on this batch (creation: its stream)
+  hipEvent_t ev = nullptr;
 
   // natoms: atoms per crystal; max_pairs 1 (plain decoder calls) or 2 (CFG pairs, sampling); knn: the
   // reference's radius graph instead of fc edges (max_neighbors as CSPNet's)
@@ -114,9 +125,24 @@ struct Batch : torch::CustomClassHolder {
                 chm_batch_device(b), ", the model is on ", model->device);
     N = chm_batch_num_nodes(b);
     E = chm_batch_num_edges(b);
+    last = (hipStream_t)stream();
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "Batch: hipEventCreate failed");
   }
   ~Batch() override {
     if (b) chm_batch_destroy(b);
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  // called under the device guard, before an op launches on the current stream: order it behind the work of the
+  // batch's last stream and keep the workspace alive for this stream (caching allocator)
+  void use_current_stream() {
+    // (the CUDA-typed view of the HIP stream: PyTorch-ROCm's caching allocator keys streams as CUDA)
+    const c10::hip::HIPStreamMasqueradingAsCUDA cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+    std::lock_guard<std::mutex> lk(mu);
+    if (cur.stream() == last) return;
+    TORCH_CHECK(hipEventRecord(ev, last) == hipSuccess && hipStreamWaitEvent(cur.stream(), ev, 0) == hipSuccess,
+                "Batch: ordering the batch's previous stream before this one failed");
+    workspace.record_stream(cur.unwrap());
+    last = cur.stream();
   }
   const chm_dims& dims() const { return model->d; }
   const c10::Device& device() const { return model->device; }
@@ -200,6 +226,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> decoder_forward(const
   const float* te = film ? fptr_on(time_emb, b, "time_emb") : nullptr;
   const float* tx = d.text_dim > 0 ? fptr_on(text, b, "text") : nullptr;
   HIPGuardMasqueradingAsCUDA guard(b.device());
+  bp->use_current_stream();
   auto o = frac.options();
   at::Tensor types = at::empty({pairs, b.N, d.max_atoms}, o), latt = at::empty({pairs, b.B, 3, 3}, o),
              coords = at::empty({pairs, b.N, 3}, o), nodes = at::empty({pairs, b.N, d.hidden_dim}, o);
@@ -254,6 +281,7 @@ void sample_step(const c10::intrusive_ptr<Batch>& bp, const c10::intrusive_ptr<S
   io.d_rand_x1 = fptr_on(rand_x1, b, "rand_x1"); io.n_rand_x1 = noise ? rand_x1->numel() : 0;
   io.d_rand_x2 = fptr_on(rand_x2, b, "rand_x2"); io.n_rand_x2 = noise ? rand_x2->numel() : 0;
   HIPGuardMasqueradingAsCUDA guard(b.device());
+  bp->use_current_stream();
   check(chm_sample_step(b.b, &sc.s, (int)t, (float)cond_scale, &io, (uint64_t)seed, node_base, graph_base, stream()),
         "chm_sample_step");
 }
@@ -266,6 +294,7 @@ at::Tensor segment_mean(const c10::intrusive_ptr<Batch>& bp, int64_t pairs, cons
   need_on(msg, b.device(), at::kFloat, "msg");
   need_shape(msg, {pairs, b.E, b.dims().hidden_dim}, "msg");
   HIPGuardMasqueradingAsCUDA guard(b.device());
+  bp->use_current_stream();
   at::Tensor agg = at::empty({pairs, b.N, b.dims().hidden_dim}, msg.options());
   check(chm_segment_mean(b.b, (int)pairs, msg.data_ptr<float>(), msg.numel(), agg.data_ptr<float>(), agg.numel(),
                          stream()),

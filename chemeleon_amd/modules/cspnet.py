@@ -222,7 +222,9 @@ class CSPNet(nn.Module):
             _lib.check(_lib.load().chm_model_set_option(self.hip_model().handle, key.encode(), int(value)),
                        "chm_model_set_option")
             self._options[key] = int(value)
-            if key == "node_ps":  # (a batch carves the pre-split operand buffers only when created with it)
+            # (a batch carves the pre-split operand buffers only when created with node_ps, and plans its
+            # pair-grid job lists with the edge_lag of its creation: cached batches are rebuilt)
+            if key in ("node_ps", "edge_lag"):
                 self._batches.clear()
 
     def set_math(self, mode: str):

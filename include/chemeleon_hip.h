@@ -85,7 +85,8 @@ void chm_model_destroy(chm_model* m);
  *     grid, run that round in one grid with the edge-layer-2 tiles that do not read its rows.
  *   "edge16" (1): accepted for compatibility (the round-1 32x32x16 kernels were removed; 0 fails).
  *   "edge_rows", "edge_layer", "edge_layer_dyn", "edge_pool", "edge_lag", "edge_layer_min": edge-layer
- *     schedules (bit-identical).
+ *     schedules (bit-identical). A batch plans its pair-grid job lists (and sizes their
+ *     buffers) with the edge_lag of its creation: a later change reaches batches created after it only.
  *   "node_ps" (0 / 1): split16 node GEMMs read their A operands pre-split by the producing kernels (not
  *     bit-identical to 0: within fp32 rounding; DESIGN.md §4 "Node GEMMs"); a batch carves their buffers only
  *     when created while the option is set (batches created without it keep the in-loop split).
@@ -309,7 +310,11 @@ int chm_segment_mean(chm_batch* b, int pairs, const float* d_msg, int64_t msg_co
  * tables with them and raises otherwise): the kernel checks them on the device,
  * and an out-of-range index makes the call return CHM_E_ARG with chm_last_error()
  * naming the first offending node (its d_out entry is -1). The check needs the
- * result, so this entry point synchronises `stream` before returning. */
+ * result, so this entry point synchronises `stream` before returning, except while
+ * `stream` is capturing a graph: then nothing is read back and the call returns at
+ * once; out-of-range nodes are the d_out entries of -1 (the flag word the check uses
+ * is allocated per host thread and device by the first, uncaptured call:
+ * CHM_E_UNSUPPORTED if the first call on a thread is captured). */
 int chm_d3pm_sample(int N, int A, int T, const float* d_logits, const int64_t* d_xt, const int64_t* d_t,
                     const float* d_noise, const float* d_q_one_step, const float* d_q_mats, int64_t* d_out,
                     void* stream);

@@ -182,6 +182,60 @@ def test_d3pm_sample_op_refuses_out_of_range_indices(model, chem, golden):
             chem.d3pm_sample(lg, xx, tt, u, q1, qm)
 
 
+def test_batch_used_from_two_streams_is_ordered(model, chem, tmodel):
+    """One Batch drives two independent samplers, one per stream, with no ordering between the streams from the
+    caller: each op waits for the previous stream's work on the batch's scratch, so both trajectories
+    equal the same steps run alone."""
+    c, n = _cond(model)
+    sched = ops.schedule(model, 1e-5)
+    states = [_state(6), _state(7)]
+    refs = []
+    b0 = _batch(tmodel, NAT, 2)
+    for a, x, lat in states:
+        ra, rx, rl = a.clone(), x.clone(), lat.clone()
+        for t in (60, 59, 58):
+            chem.sample_step(b0, sched, t, 2.0, ra, rx, rl, c, n, None, None, None, None, 7, 0, 0)
+        refs.append((ra, rx, rl))
+    torch.cuda.synchronize()
+    b = _batch(tmodel, NAT, 2)  # (built on the default stream)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    work = [tuple(v.clone() for v in st) for st in states]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())  # (the inputs are ready)
+    for t in (60, 59, 58):
+        for s, (ga, gx, gl) in zip(streams, work):
+            with torch.cuda.stream(s):
+                chem.sample_step(b, sched, t, 2.0, ga, gx, gl, c, n, None, None, None, None, 7, 0, 0)
+    torch.cuda.synchronize()
+    for (ga, gx, gl), (ra, rx, rl) in zip(work, refs):
+        assert torch.equal(ga, ra) and torch.equal(gx, rx) and torch.equal(gl, rl)
+
+
+def test_d3pm_sample_op_under_graph_capture(model, chem, golden):
+    """chm_d3pm_sample captured into a graph: no host sync in the capture; the replay gives the
+    eager result, and an out-of-range node is marked -1 in the output instead of raising."""
+    g = golden("units.npz")
+    dp = model.d3pm
+    lg, xt, t, u = [torch.from_numpy(g[k]).to(DEV) for k in ("d3pm_logits", "d3pm_xt", "d3pm_t", "d3pm_u")]
+    q1, qm = dp.q_one_step_mats.contiguous(), dp.q_mats.contiguous()
+    chem.d3pm_sample(lg, xt, t, u, q1, qm)  # (the first call on this thread allocates the check's flag word)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            out = chem.d3pm_sample(lg, xt, t, u, q1, qm)
+    graph.replay()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), g["d3pm_out"])
+    t[2] = qm.shape[0]  # t = T + 1: out of range
+    graph.replay()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert got[2] == -1
+    np.testing.assert_array_equal(np.delete(got, 2), np.delete(g["d3pm_out"], 2))
+
+
 def test_ops_check_shapes_and_devices_before_launch(model, chem, tmodel):
     """Every tensor is checked against the batch's sizes, the model's dimensions and the batch's device on
     the host: a mis-sized tensor or one on another device raises RuntimeError and nothing is launched."""
