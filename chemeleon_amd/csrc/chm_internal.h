@@ -58,6 +58,7 @@ enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 // split16 edge GEMMs (edge16.hip): both operands split into fp16 hi/lo, stored per row as
 // [K/32][hi 32 | lo 32] (a 32-deep K-tile of a row = one 128-B line), three fp16 MFMA products,
 // staged by global_load_lds.
+constexpr int kPairRows = 128;  // pairs per tile of edge layer 1 on pairs (k_edge16_pairs / the pair grid)
 constexpr int kRowInfo = 260;  // EdgeArgs::rinfo entries per row tile (a tile holds at most 257 nodes)
 struct EdgeArgs {
   long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M)
@@ -111,6 +112,9 @@ struct EdgeArgs {
   // features (Mp rows: per crystal the pairs i <= j, row-major), pi / pj = the pair's nodes, pe = its edge
   // rows {(i, j), (j, i)} (equal for i == j)
   const int* pi; const int* pj; const int2* pe; long Mp;
+  // per pair tile (kPairRows pairs): {first node, node count} of the P / Q rows its epilogue reads (the tile's
+  // first pair's i up to the end of the crystal of its last pair), staged in LDS when they fit
+  const int2* pnode;
   unsigned long long* trace;  // profiling: per block {hw id, t0, t_mainloop, t_end} (s_memrealtime) or null
   int stagger;  // first-round start delay (units of s_sleep 127) of every other CU, 0 = none
   int dbg;  // profiling ablations (0 in the product; wrong results): bit 0 = no K-loop loads, bit 1 = no

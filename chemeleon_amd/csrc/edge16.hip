@@ -1101,6 +1101,11 @@ constexpr int P_NSA = 3, P_NSW = 2;      // ring depths: A (streamed), W (L2-res
 constexpr int P_OPA = PBM * ROW_B;       // 16 KB per A stage
 constexpr int P_WRING = P_NSA * P_OPA;   // W stages follow the A stages (32 KB each)
 static_assert(P_WRING + P_NSW * OPND_B <= LDS_B, "LDS");
+static_assert(PBM == kPairRows, "pair tile rows (host tables)");
+// the epilogue's staged P / Q rows: per node [P 256 | Q 256 | 8 pad] floats of this column tile (a pitch of 8
+// dwords mod 64 banks: the 16 lanes of a ds_read_b128 group, rows of consecutive nodes, hit distinct banks)
+constexpr int P_QP = 520;
+constexpr int P_QROWS = LDS_B / (P_QP * 4);  // 78 node rows
 }  // namespace
 
 // one pair tile: bid = pair tile * 2 + column tile (tid_in: the persistent kernel's opaque copy of threadIdx.x)
@@ -1200,6 +1205,9 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
     __builtin_amdgcn_sched_group_barrier(0x008, 12 - 2 * nr, 0);
   };
 
+  // the node range of the epilogue's P / Q rows (one load, issued ahead of the operand stream: in by tile 0)
+  int2 pqn = {0, 0};
+  if (g.pnode) pqn = g.pnode[row0 / PBM];
   // prologue (issue order W0 A0 A1 W1 A2): tile 0 has landed when 8 glds remain (A1 2, W1 4, A2 2)
   issueW(0);
   issueA(0);
@@ -1209,6 +1217,8 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  // (block-uniform: SGPRs across the main loop)
+  const int q_lo = __builtin_amdgcn_readfirstlane(pqn.x), q_n = __builtin_amdgcn_readfirstlane(pqn.y);
   read_A(0, 0);
   read_W(0, 0, 0);
 
@@ -1279,6 +1289,24 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
   }
 
   // ---- epilogue: undo the W row scales, then per conditioning and direction S = SiLU(U +- V + P + Q)
+  // The P / Q rows of the tile's nodes [q_lo, q_lo + q_n) are staged in LDS (global_load_lds, one latency for all
+  // of them instead of one per conditioning, direction and row group): both conditionings when they fit, else
+  // conditioning 0's; more nodes than P_QROWS (crystals of 78+ atoms): all read from global memory.
+  const bool stg = g.pnode && q_n <= P_QROWS && !(g.dbg & 1048576);  // (dbg 1048576: profiling, never staged)
+  const bool both = stg && g.npairs * q_n <= P_QROWS;
+  auto stage_pq = [&](int c0, int c1) __attribute__((always_inline)) {
+    for (int c = c0; c < c1; ++c) {
+      const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H) + n0 + 4 * lane;
+      const int rb = both ? c * q_n : 0;
+      for (int r = wave; r < q_n; r += 8) {
+        const float* src = Pc + (long)(q_lo + r) * (2 * H);
+        char* dst = lds + (rb + r) * (P_QP * 4);
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)(src + H), (lds_void*)(dst + BN * 4), 16, 0, 0);
+      }
+    }
+  };
+  if (stg) stage_pq(0, both ? g.npairs : 1);  // (lands while the scales and the pair tables load)
   const int cw = n0 + wn * 128 + 4 * g4;  // this lane's first output column (+ 16 j)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -1301,19 +1329,33 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
     pe[i] = g.pe[p];
     ok[i] = lr < nrows;
   }
+  if (stg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
   const bool odd = l16 & 1;
   const bool nostore = g.dbg & 4;  // (profiling)
-  for (int c = 0; c < g.npairs; ++c) {
+  const float* T = reinterpret_cast<const float*>(lds);
+  auto conditioning = [&](int c, auto STG) __attribute__((always_inline)) {
+    constexpr bool staged = decltype(STG)::value;
     const float* Pc = g.PQ + (long)c * g.nnodes * (2 * H);
+    const int rb = both ? c * q_n : 0;
     static_for<0, 2>([&](auto DIR) __attribute__((always_inline)) {
       constexpr int dir = decltype(DIR)::value;
       static_for<0, 2>([&](auto IC) __attribute__((always_inline)) {
         constexpr int i = decltype(IC)::value;
         // forward (i, j): P_i + Q_j, row pe.x; reverse (j, i): P_j + Q_i, row pe.y (none for a self pair)
         const int rp = dir ? nj[i] : ni[i], rq = dir ? ni[i] : nj[i];
-        const float* prow = Pc + (long)rp * (2 * H) + cw;
-        const float* qrow = Pc + (long)rq * (2 * H) + H + cw;
+        const float* prow;
+        const float* qrow;
+        if constexpr (staged) {
+          prow = T + (rb + rp - q_lo) * P_QP + wn * 128 + 4 * g4;
+          qrow = T + (rb + rq - q_lo) * P_QP + BN + wn * 128 + 4 * g4;
+        } else {
+          prow = Pc + (long)rp * (2 * H) + cw;
+          qrow = Pc + (long)rq * (2 * H) + H + cw;
+        }
         // (dbg 131072 / 262144, profiling: no reverse-direction stores / the reverse rows stored at the forward
         // rows' places: what the scattered reverse rows cost; wrong results)
         const long orow = (long)c * g.E + (dir && !(g.dbg & 262144) ? pe[i].y : pe[i].x);
@@ -1369,12 +1411,20 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
           if (st_e) *reinterpret_cast<f16x8*>(se + cc * 64) = odd ? r8 : hv;  // even lane's row: hi (even), lo (odd)
           if (st_o) *reinterpret_cast<f16x8*>(so + cc * 64) = odd ? lv : r8;  // odd lane's row
         }
-        if (st && g4 == 0) {
+        if (st && g4 == 0 && !(g.dbg & 2097152)) {  // (dbg 2097152, profiling: no exponent bytes; wrong results)
           signed char* px = reinterpret_cast<signed char*>(g.sexp) + orow * 4 + (n0 + wn * 128) / CHUNK;
           *px = (signed char)ex2;
         }
       });
     });
+  };
+  // (only conditioning 0's rows staged: conditioning 1 reads its rows from global memory, since staging them
+  // now would have to wait for conditioning 0's S stores too: vmcnt counts loads and stores in one counter)
+  for (int c = 0; c < g.npairs; ++c) {
+    if (stg && (c == 0 || both))
+      conditioning(c, std::integral_constant<bool, true>{});
+    else
+      conditioning(c, std::integral_constant<bool, false>{});
   }
 }
 

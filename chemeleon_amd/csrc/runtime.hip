@@ -112,6 +112,7 @@ struct chm_batch {
   // fc: the unordered pairs (i <= j) of every crystal for edge layer 1 on pairs (BatchTables::pi / pj / pe)
   int *pi = nullptr, *pj = nullptr;
   int2* pe = nullptr;
+  int2* pnode = nullptr;  // per pair tile: the node range of its P / Q rows (EdgeArgs::pnode)
   long Ep = 0;
   // fc, split16: the job lists of both edge layers in one static grid on pairs (k_edge16_pairs_grid), built for
   // P = max_pairs and the model's edge_lag at creation; per layer 8 npx pair-tile flags (psched)
@@ -508,6 +509,10 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_dbg = value ? (m->edge_dbg | 16384) : (m->edge_dbg & ~16384);
     return CHM_OK;
   }
+  if (k == "edge_pairs_pq_global") {  // (tests) the pair epilogue reads its P / Q rows from global memory (no LDS staging)
+    m->edge_dbg = value ? (m->edge_dbg | 1048576) : (m->edge_dbg & ~1048576);
+    return CHM_OK;
+  }
   if (k == "edge_rows_nowait") {  // (tests) row tiles never wait for the previous tile: the msgbuf path
     m->edge_dbg = value ? (m->edge_dbg | 64) : (m->edge_dbg & ~64);
     return CHM_OK;
@@ -552,7 +557,7 @@ struct BatchTables {
   long N = 0, E = 0;  // knn: E = the edge capacity
   // fc: the unordered pairs i <= j of every crystal, row-major (edge layer 1 on pairs, k_edge16_pairs)
   std::vector<int> pi, pj;
-  std::vector<int2> pe;
+  std::vector<int2> pe, pnode;
   long Ep = 0;
   long C = 0;         // knn: candidate scratch entries (sum of n^2 * 27)
   bool knn = false;
@@ -680,6 +685,14 @@ static void batch_fill(BatchTables& t) {
         t.pe[p] = make_int2((int)(t.eoff[g] + (long)i * n + j), (int)(t.eoff[g] + (long)j * n + i));
       }
   }
+  // the pair tiles' P / Q node ranges: from the first pair's i (pairs are ordered by crystal, then i <= j, so every
+  // node of the tile is >= it) to the end of the crystal of the last pair (every j of the tile is below it)
+  t.pnode.resize((t.Ep + kPairRows - 1) / kPairRows);
+  for (size_t k = 0; k < t.pnode.size(); ++k) {
+    const long p0 = (long)k * kPairRows, p1 = std::min<long>(p0 + kPairRows, t.Ep) - 1;
+    const int gl = t.n2g[t.pi[p1]];
+    t.pnode[k] = make_int2(t.pi[p0], t.noff[gl] + t.nat[gl] - t.pi[p0]);
+  }
   t.ei.resize(E);
   t.ej.resize(E);
   t.estart.resize(N);
@@ -751,6 +764,7 @@ static size_t batch_layout(chm_batch* b, const chm_model* m, char* base, long nt
     b->pi = (int*)carve(b->Ep * sizeof(int));
     b->pj = (int*)carve(b->Ep * sizeof(int));
     b->pe = (int2*)carve(b->Ep * sizeof(int2));
+    b->pnode = (int2*)carve((b->Ep + kPairRows - 1) / kPairRows * sizeof(int2));
   }
   if (!b->pplan.jobs.empty()) {  // (and the one-grid pair schedule: job lists, ranges, per-layer words)
     b->pjobs = (int4*)carve(b->pplan.djobs.size() * sizeof(int4));
@@ -901,6 +915,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
     up(b->pi, t.pi.data(), t.pi.size() * sizeof(int));
     up(b->pj, t.pj.data(), t.pj.size() * sizeof(int));
     up(b->pe, t.pe.data(), t.pe.size() * sizeof(int2));
+    up(b->pnode, t.pnode.data(), t.pnode.size() * sizeof(int2));
     if (b->pjobs) {
       up(b->pjobs, b->pplan.djobs.data(), b->pplan.djobs.size() * sizeof(int4));
     }
@@ -1373,7 +1388,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       if (pair_grid) {
         // both edge layers in one grid, layer 1 on pairs (k_edge16_pairs_grid)
         EdgeArgs e1p = e1;
-        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
+        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe; e1p.pnode = b->pnode;
         e1p.xbad = e2.xbad = b->xbad + l;
         PairSched ps;
         ps.jobs = b->pjobs; ps.jstride = b->pplan.jstride;
@@ -1390,7 +1405,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
       } else if (pairs) {
         // edge layer 1 on pairs (both directions' S rows per pair), then edge layer 2 on its row tiles
         EdgeArgs e1p = e1;
-        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe;
+        e1p.M = b->Ep; e1p.Mp = b->Ep; e1p.pi = b->pi; e1p.pj = b->pj; e1p.pe = b->pe; e1p.pnode = b->pnode;
         {
           ProfScope ps(CHM_K_EDGE_FOURIER, s);
           HIPCHK(edge_gemm16_pairs(e1p, s));

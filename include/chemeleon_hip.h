@@ -98,7 +98,8 @@ void chm_model_destroy(chm_model* m);
  *   The persistent one-grid kernel (edge_layer_dyn) runs only where model creation saw 8 XCDs ("xcd_mask" =
  *     0xff); tests: "edge_dyn_skip_xcd" (its blocks on one XCD exit, the launch's self-check must raise the
  *     repair), "edge_layer_repair", "edge_tail_timeout", "edge_tail_norepair" (WRONG results after a
- *     timeout), "edge_rows_nowait".
+ *     timeout), "edge_rows_nowait", "edge_pairs_pq_global" (the pair epilogue's P / Q rows from global memory
+ *     instead of LDS).
  * Returns CHM_E_ARG for an unknown key. */
 int chm_model_set_option(chm_model* m, const char* key, int64_t value);
 

@@ -945,3 +945,32 @@ def test_edge_pairs_grid_is_bit_identical(cn, nat):
     for k, name in ((1, "static grid"), (2, "static grid + forced repair")):
         for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
             assert torch.equal(u, v), f"{what}: {name} differs from the two-launch pair schedule"
+
+
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [79, 78, 2, 80]])
+def test_pair_epilogue_staged_rows_are_bit_identical(cn, nat):
+    """The pair tiles' epilogue stages the P / Q rows of their nodes in LDS (both conditionings when they fit,
+    else conditioning 0; tiles of more than 78 nodes read global memory): the same values in the same
+    arithmetic, so one reverse step equals the unstaged form ('edge_pairs_pq_global') bit for bit, in the
+    two-launch schedule and in the pair grid. The shapes mix tiles of one and two crystals, of 1-atom crystals,
+    and of 78-80-atom crystals (staged and global at the size limit)."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(23)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    model = _model(1000)
+    model.decoder.set_option("edge_pairs", 1)
+    model.decoder.set_option("edge_layer_min", 1)
+    outs = []
+    for form, glob in ((0, 1), (0, 0), (1, 0)):
+        model.decoder.set_option("edge_pairs_layer", form)
+        model.decoder.set_option("edge_pairs_pq_global", glob)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+    del model
+    torch.cuda.empty_cache()
+    for k, name in ((1, "two launches, staged"), (2, "pair grid, staged")):
+        for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
+            assert torch.equal(u, v), f"{what}: {name} differs from the unstaged pair epilogue"
