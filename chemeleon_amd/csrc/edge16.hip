@@ -1566,8 +1566,13 @@ __global__ __launch_bounds__(512, 1) void k_edge16_pairs_grid(EdgeArgs g1, EdgeA
   if (j.x == 1) {
     pair_tile(g1, j.y, threadIdx.x);
     // every store of this tile has reached the XCD's L2; count the column tile (and a misplaced block)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // (dbg 4194304, profiling: published without waiting for the stores, the drain's cost; wrong results)
+    if (!(g1.dbg & 4194304)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_s_barrier();  // (an LDS-only barrier: __syncthreads() would wait for the stores)
+    }
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(pf + j.z, 1u + ((me + 1u) << (8 + 4 * (j.y & 1))), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
