@@ -6,10 +6,11 @@ edges inside a crystal only), so the path shards without any per-step
 exchange:
   1. rank 0 computes the conditioning vectors once (the frozen text encoder)
      and broadcasts them (2 x [B, 512] fp32);
-  2. every rank samples a contiguous range of crystals, balanced by edge work
-     (sum of n^2). The noise never depends on the number of ranks: in parity
-     mode (noise="torch", the reference's CPU RNG stream) every rank advances
-     the CPU generator over the global draws and keeps its own rows
+  2. every rank samples a contiguous range of crystals, balanced by work
+     (sum of n^2 + NODE_COST * n: edges and atoms). The noise never
+     depends on the number of ranks: in parity mode (noise="torch", the
+     reference's CPU RNG stream) every rank advances the CPU generator
+     over the global draws and keeps its own rows
      (chemeleon_amd.noise); in perf mode (noise="philox") device Philox noise
      is keyed by GLOBAL node / graph index;
   3. the finished structures are all-gathered (padded to the largest shard).
@@ -26,17 +27,23 @@ import torch
 import torch.distributed as dist
 
 
+# per-atom cost of a crystal in units of one fc edge (n^2 edges, n atoms): the node-side work (FiLM, the per-node
+# halves of edge layer 1, the node MLP: per-row GEMMs at small M) fitted on the eight ranks' shares of configs[4]
+# run one by one on one MI355X (profiles/r6/share: ms per step = 7.66e-5 sum n^2 + 1.28e-3 sum n + c, ratio 16.7)
+NODE_COST = 16
+
+
 def partition(natoms: Sequence[int], world: int) -> List[Tuple[int, int]]:
-    """Contiguous [g0, g1) crystal ranges per rank with roughly equal sum of
-    n^2 (the fc edge work). Every rank gets at least one crystal; fewer
-    crystals than ranks is an error."""
+    """Contiguous [g0, g1) crystal ranges per rank with roughly equal work,
+    sum of n^2 + NODE_COST * n (fc edges and atoms). Every rank gets at least
+    one crystal; fewer crystals than ranks is an error."""
     natoms = [int(n) for n in natoms]
     G = len(natoms)
     if G < max(world, 1):
         raise ValueError(f"{G} crystals cannot be sharded over {world} ranks (one crystal at least per rank)")
     if world <= 1:
         return [(0, G)]
-    w = [n * n for n in natoms]
+    w = [n * n + NODE_COST * n for n in natoms]
     total = float(sum(w))
     bounds, acc, g = [0], 0.0, 0
     for r in range(1, world):

@@ -21,7 +21,8 @@ def test_partition_balances_edge_work():
     g = torch.Generator().manual_seed(7)
     rag = torch.randint(1, 81, (2048,), generator=g).tolist()
     parts = partition(rag, 8)
-    work = [sum(n * n for n in rag[a:b]) for a, b in parts]
+    from chemeleon_amd.distributed import NODE_COST
+    work = [sum(n * n + NODE_COST * n for n in rag[a:b]) for a, b in parts]
     assert max(work) / min(work) < 1.02
     assert [p[1] for p in parts[:-1]] == [p[0] for p in parts[1:]]
     assert partition([5, 5, 5], 3) == [(0, 1), (1, 2), (2, 3)]
