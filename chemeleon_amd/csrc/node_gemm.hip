@@ -243,6 +243,34 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
       __builtin_amdgcn_global_load_lds((gbl_void*)(wsrc[u] + (S16 ? 2 * k0 : k0)), (lds_void*)(st + wdst[u]), 16, 0, 0);
   };
 
+  // Short grids (64-row split16 tiles, one to two blocks per CU and nothing else to run): the epilogue's per-column
+  // vectors (W scales, bias or the per-graph row terms, and on 64 x 64 tiles the residual rows) are loaded here,
+  // ahead of the operand stream, so their latency runs under the K loop instead of opening the epilogue (the same
+  // values in the same expressions: bit-identical)
+  constexpr bool PRE = S16 && !PS && NMT == 64 && (NNT == 64 || NB == 3), PRE_R = PRE && NNT == 64;
+  f32x4 pws[PRE ? NJ : 1][4], pv2[PRE ? NJ : 1][4], prr[PRE_R ? NJ : 1][4];
+  bool pre_gb = false;
+  if constexpr (PRE) {
+    static_assert(NI == 1, "one row per lane");
+    const long lr = wm * (NM / 2) + r32;
+    const long prow_ = row0 + (lr < nrows ? lr : nrows - 1);
+    pre_gb = !g.bias && g.gb;
+    const float* gbrow = pre_gb ? g.gb + (long)g.row2g[prow_ % g.gb_rowmod] * g.ldgb : nullptr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn * (NNT / 2) + j * 32 + 8 * q + 4 * h;
+        pws[j][q] = *reinterpret_cast<const f32x4*>(g.wscale + col);
+        if (g.bias)
+          pv2[j][q] = *reinterpret_cast<const f32x4*>(g.bias + col);
+        else if (gbrow && col < g.gb_cols)
+          pv2[j][q] = *reinterpret_cast<const f32x4*>(gbrow + col);
+        if constexpr (PRE_R)
+          if (g.R) prr[j][q] = *reinterpret_cast<const f32x4*>(g.R + prow_ * g.ldr + col);
+      }
+  }
+
   f32x16 acc[NI][NJ];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
@@ -451,7 +479,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     float cm = 0.f;  // max |C| over this lane's columns of the row
     if (lr < nrows) {
       const long row = row0 + lr;
-      const float* gbrow = g.gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
+      const float* gbrow = g.gb && !pre_gb ? g.gb + (long)g.row2g[row % g.gb_rowmod] * g.ldgb : nullptr;
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -460,13 +488,24 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
           f32x4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-          if constexpr (S16) v *= *reinterpret_cast<const f32x4*>(g.wscale + col) * aun[i];  // undo the scales
-          if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
-          if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+          if constexpr (PRE) {
+            v *= pws[j][q] * aun[i];  // undo the scales
+            if (g.bias) v += pv2[j][q];
+            if (pre_gb && col < g.gb_cols) v += pv2[j][q];
+            if (!pre_gb && gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);  // (bias and gb)
+          } else {
+            if constexpr (S16) v *= *reinterpret_cast<const f32x4*>(g.wscale + col) * aun[i];  // undo the scales
+            if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+            if (gbrow && col < g.gb_cols) v += *reinterpret_cast<const f32x4*>(gbrow + col);
+          }
           if (g.act == 1)
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = silu_n(v[e]);
-          if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+          if constexpr (PRE_R) {
+            if (g.R) v += prr[j][q];
+          } else {
+            if (g.R) v += *reinterpret_cast<const f32x4*>(g.R + row * g.ldr + col);
+          }
           *reinterpret_cast<f32x4*>(g.C + row * g.ldc + col) = v;
           if constexpr (S16) cm = fmaxf(cm, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
