@@ -80,7 +80,7 @@ struct chm_model {
   int edge_split = 1;    // CHM_EDGE_SPLIT=0: no partial-round tail split of edge layer 1 (see run_decoder)
   int edge_rows = 1;     // CHM_EDGE_ROWS=0: edge layer 2 on node-aligned segment tiles instead of row tiles
   int edge_layer = 1;    // CHM_EDGE_LAYER=0: edge layers 1 and 2 as two launches (else one grid, k_edge16_layer)
-  int edge_lag = 10;     // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD
+  int edge_lag = 8;      // CHM_EDGE_LAG: its layer-2 lag behind layer 1, in row tiles per XCD (pair grid: pair tiles; r6: 8)
   long edge_layer_min = kLayerMinTiles;  // CHM_EDGE_LAYER_MIN: row tiles from which the one-grid kernel runs
   int edge_dyn = 1;      // CHM_EDGE_DYN: one-grid kernel form, 0 static block -> job map (k_edge16_layer), 1 the
                          // persistent form (k_edge16_layer_dyn) from kDynMinTiles row tiles on, 2 always persistent
