@@ -119,6 +119,7 @@ SIGNATURES = {
     "chm_debug_pair_plan": (c_i64, [ctypes.POINTER(ctypes.c_int32), c_int, c_int, c_int, ctypes.POINTER(ctypes.c_int32),
                                     c_i64, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), c_i64]),
+    "chm_debug_pair_nodes": (c_i64, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64]),
     "chm_debug_row_nodes": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64,
                                     ctypes.POINTER(ctypes.c_int32), c_i64]),
     "chm_debug_row_tiles": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64,

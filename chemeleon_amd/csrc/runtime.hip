@@ -1061,6 +1061,18 @@ extern "C" int64_t chm_debug_pair_plan(const int32_t* h_natoms, int B, int P, in
   return pl.jstride;
 }
 
+// (host only, tests) the pair tiles' P / Q node ranges of an fc batch: see include/chemeleon_hip.h
+extern "C" int64_t chm_debug_pair_nodes(const int32_t* h_natoms, int B, int32_t* out, int64_t cap) {
+  if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad arguments");
+  BatchTables t;
+  if (int rc = batch_tables(h_natoms, B, t)) return rc;
+  batch_fill(t);
+  const int64_t NP = (int64_t)t.pnode.size();
+  if (out && cap >= 2 * NP)
+    for (int64_t k = 0; k < NP; ++k) { out[2 * k] = t.pnode[k].x; out[2 * k + 1] = t.pnode[k].y; }
+  return NP;
+}
+
 extern "C" int chm_batch_device(const chm_batch* b) { return b ? b->m->device : fail(CHM_E_ARG, "batch is NULL"); }
 extern "C" int chm_batch_info(const chm_batch* b, chm_dims* dims, int64_t* num_graphs, int* max_pairs, int* knn) {
   if (!b) return fail(CHM_E_ARG, "batch is NULL");

@@ -362,6 +362,10 @@ int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out);
  * tile)}. */
 int64_t chm_debug_pair_plan(const int32_t* h_natoms, int B, int P, int lag, int32_t* rng, int64_t cap_rng, int32_t* pa,
                             int32_t* pb, int32_t* njobs, int32_t* jobs, int64_t cap_jobs);
+/* Host-only test hook: per pair tile (128 unordered pairs i <= j of an fc batch, crystal-major) the node range
+ * [out[2k], out[2k] + out[2k+1]) whose P / Q rows its epilogue stages in LDS (edge layer 1 on pairs). Returns the
+ * number of pair tiles (or a negative CHM_E_*); out is filled when cap >= 2 x that number. */
+int64_t chm_debug_pair_nodes(const int32_t* h_natoms, int B, int32_t* out, int64_t cap);
 /* Fourier edge features of this batch's fc edges (cspnet.py:38-52,324):
  * d_frac [N,3] -> d_feat [E, 6*num_freqs]. */
 int chm_edge_features(chm_batch* b, const float* d_frac, float* d_feat, void* stream);

@@ -88,3 +88,34 @@ def test_pair_plan_covers_every_row_tile_with_its_pairs(nat):
             if jobs[x, k, 0] == 2:
                 counts[jobs[x, k, 1] // (2 * P)] += 1
     assert (counts == 2 * P).all()
+
+
+@pytest.mark.parametrize("nat", [[40] * 64, [23, 7, 40, 1, 80] * 23, [1] * 300 + [2] * 70 + [3] * 9, [5, 9, 3],
+                                 [80] * 9, [79, 78, 2, 80], list(np.random.default_rng(7).integers(1, 81, 256))])
+def test_pair_tile_node_ranges_cover_their_pairs(nat):
+    """The node range each pair tile's epilogue stages (chm_debug_pair_nodes, batch creation): every node i and j
+    of the tile's pairs lies inside it, and it starts at the tile's first node (no row is staged below it)."""
+    nat = [int(n) for n in nat]
+    L = _lib.load()
+    arr = (ctypes.c_int32 * len(nat))(*nat)
+    NP = L.chm_debug_pair_nodes(arr, len(nat), None, 0)
+    _, Ep = pair_index(nat)
+    assert NP == (Ep + PBM - 1) // PBM
+    out = (ctypes.c_int32 * (2 * NP))()
+    assert L.chm_debug_pair_nodes(arr, len(nat), out, 2 * NP) == NP
+    rng = np.array(out).reshape(NP, 2)
+    # the pairs' nodes, crystal-major, row-major i <= j
+    off = np.concatenate([[0], np.cumsum(nat)])
+    pi, pj = [], []
+    for g, n in enumerate(nat):
+        for i in range(n):
+            for j in range(i, n):
+                pi.append(off[g] + i)
+                pj.append(off[g] + j)
+    pi, pj = np.array(pi), np.array(pj)
+    for k in range(NP):
+        a, b = k * PBM, min(Ep, k * PBM + PBM)
+        lo, n = rng[k]
+        nodes = np.concatenate([pi[a:b], pj[a:b]])
+        assert lo == pi[a] and nodes.min() == lo and nodes.max() < lo + n, f"pair tile {k}: [{lo}, {lo + n})"
+        assert n >= 1 and lo + n <= off[-1]
