@@ -124,6 +124,12 @@ SIGNATURES = {
                                     ctypes.POINTER(ctypes.c_int32), c_i64]),
     "chm_debug_row_tiles": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, ctypes.POINTER(ctypes.c_int32), c_i64,
                                     ctypes.POINTER(c_i64)]),
+    "chm_debug_row_nodes_ex": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, c_i64, ctypes.POINTER(ctypes.c_int32),
+                                       c_i64, ctypes.POINTER(ctypes.c_int32), c_i64]),
+    "chm_debug_row_tiles_ex": (c_int, [ctypes.POINTER(ctypes.c_int32), c_int, c_i64, ctypes.POINTER(ctypes.c_int32),
+                                       c_i64, ctypes.POINTER(c_i64)]),
+    "chm_debug_short_row_tiles": (c_i64, [ctypes.POINTER(ctypes.c_int32), c_int, c_int, c_int, c_i64]),
+    "chm_batch_short_row_tiles": (c_i64, [c_void_p]),
     "chm_batch_device_bytes": (ctypes.c_size_t, [c_void_p]),
     "chm_batch_num_nodes": (c_i64, [c_void_p]),
     "chm_batch_num_edges": (c_i64, [c_void_p]),
@@ -166,7 +172,12 @@ def load(path: str = None):
                 "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
         lib = ctypes.CDLL(p)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                # (A/B runs load an older build through CHM_LIB: test hooks it predates stay unbound)
+                if os.environ.get("CHM_LIB") and name.startswith(("chm_debug_", "chm_batch_short")):
+                    continue
+                raise ImportError(f"chemeleon_amd: {p} does not export {name} (stale build?)")
             fn.restype = res
             fn.argtypes = args
         _lib = lib

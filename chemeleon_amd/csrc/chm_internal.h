@@ -60,6 +60,7 @@ enum { EPI_STD = 0, EPI_EDGE = 1, EPI_SEGMEAN = 2 };
 // staged by global_load_lds.
 constexpr int kPairRows = 128;  // pairs per tile of edge layer 1 on pairs (k_edge16_pairs / the pair grid)
 constexpr int kRowInfo = 260;  // EdgeArgs::rinfo entries per row tile (a tile holds at most 257 nodes)
+constexpr int kShortRows = 192;  // edge layer 2's short row tiles (a mixed tiling's last round)
 struct EdgeArgs {
   long M;                        // EPI_STD / EPI_EDGE: rows [row_base, M)
   long row_base;
@@ -93,6 +94,10 @@ struct EdgeArgs {
   // one counter per column group of 64; msgbuf [P][r2tot][H]: the continued rows, written only when
   // tile t-1 has not published in time). null rtiles = node tiles (tiles / ntiles).
   const int4* rtiles; float* sbuf; float* msgbuf; unsigned* rcnt; long r2tot;
+  // a mixed row tiling (r6, short last round): this launch runs rt_count row tiles from rt_first on (0 = all
+  // ntiles), tile rt_first + k = rows [rt_e0 + k rt_h, + rt_h) (rt_h 0 = 256); 192-row tiles run in k_edge16_short
+  // (3 row groups per wave). Tile indices stay global (rtiles, rinfo, sbuf and rcnt are indexed by them).
+  int rt_first, rt_count, rt_h; long rt_e0;
   // fc row tiles: each tile's node list as the segment-mean epilogue uses it, built on the host with the
   // batch (rinfo [ntiles][kRowInfo] {node, rows | first row << 10 | kind << 20}, rinfo_n [ntiles] entries),
   // so the epilogue loads it in one round trip instead of deriving it through dependent loads; or null

@@ -114,8 +114,12 @@ __host__ __device__ inline LayerJob layer_job(long b, long R, int P, int D) {
 // is coherent only if those layer-1 tiles ran on the same XCD: the layer-1 tiles record their XCD in
 // the flag word and a layer-2 tile that finds another one raises *xbad (the runtime's repair launches
 // then recompute the layer).
-template <int EPI, bool ASC, bool ONE = false>
+// RG: 16-row groups per wave (4: 256-row tiles; 3: edge layer 2's 192-row tiles, k_edge16_short). The operand
+// staging loads 256 A rows either way (the rows past a short tile are read, never used).
+template <int EPI, bool ASC, bool ONE = false, int RG = 4>
 __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb, long bid_in = -1, int tid_in = -1) {
+  static_assert(RG == 4 || (RG == 3 && EPI == EPI_SEGMEAN && !ONE), "short row tiles: edge layer 2's own launch");
+  constexpr int RW = 16 * RG;  // rows per wave row (wm)
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // (tid_in >= 0: the persistent kernel's opaque copy of threadIdx.x, so its loop does not hoist the
   // tile's index math out of the loop and keep it in registers)
@@ -133,10 +137,13 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     const long rest = bid / ntn;
     seg_c = (int)(rest % g.npairs);
     if (g.rtiles) {  // edge rows [256 t, 256 t + 256) of conditioning seg_c, nodes cut at the tile ends
-      rtile = rest / g.npairs;
-      const long e0 = rtile * BM;
+      // (a mixed tiling's launch: its tiles from rt_first on, rt_h rows each from row rt_e0)
+      const long tl = rest / g.npairs;
+      const long th = g.rt_h ? g.rt_h : BM;
+      rtile = g.rt_first + tl;
+      const long e0 = g.rt_e0 + tl * th;
       row0 = (long)seg_c * g.E + e0;
-      nrows = g.E - e0 < BM ? g.E - e0 : BM;
+      nrows = g.E - e0 < th ? g.E - e0 : th;
     } else {
       seg = g.tiles[rest / g.npairs];
       const long es0 = g.node_estart[seg.x];
@@ -256,20 +263,22 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     stamp(4);  // (traces of this grid: slot 4 = the wait for the layer-1 tiles is over)
   }
 
-  // ---- row exponents of the A chunks (edge layer 2): the lane's four rows
-  int ex[4] = {0, 0, 0, 0};
+  // ---- row exponents of the A chunks (edge layer 2): the lane's RG rows
+  int ex[RG];
+#pragma unroll
+  for (int i = 0; i < RG; ++i) ex[i] = 0;
   if (ASC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long lr = wm * 64 + 16 * i + l16;
+    for (int i = 0; i < RG; ++i) {
+      const long lr = wm * RW + 16 * i + l16;
       const int* pe = g.aexp + row0 + (lr < nrows ? lr : nrows - 1);
       ex[i] = *pe;
     }
   }
 
-  f32x4 acc[4][8];
+  f32x4 acc[RG][8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < RG; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -277,13 +286,13 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   // physical chunk (4p + g4) ^ swz(r); swz depends on l16 only (group bases are multiples of 16)
   const int swz = (l16 >> 1) & 7;
   const int ch0 = 16 * (g4 ^ swz), ch1 = 16 * ((4 + g4) ^ swz);
-  const int fa = (wm * 64 + l16) * ROW_B, fw = (wn * 128 + l16) * ROW_B;
-  f16x8 fA[2][2][4];  // [set][plane][row group]
+  const int fa = (wm * RW + l16) * ROW_B, fw = (wn * 128 + l16) * ROW_B;
+  f16x8 fA[2][2][RG];  // [set][plane][row group]
   f16x8 fW[2][2][2];  // [set][plane][column group of the quarter]
   auto read_A = [&](int set, int t) __attribute__((always_inline)) {
     const char* SA = lds + (t % NSA) * OPND_B + fa;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RG; ++i) {
       fA[set][0][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch0);
       fA[set][1][i] = *reinterpret_cast<const f16x8*>(SA + i * 16 * ROW_B + ch1);
     }
@@ -296,27 +305,27 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       fW[set][1][jj] = *reinterpret_cast<const f16x8*>(SW + jj * 16 * ROW_B + ch1);
     }
   };
-  // one quarter: columns 32qq .. 32qq+31 of the wave, all four row groups, three products
+  // one quarter: columns 32qq .. 32qq+31 of the wave, all RG row groups, three products
   // (small terms first: w_lo a_hi, w_hi a_lo, then w_hi a_hi)
   auto mfq = [&](int aset, int wset, int qq) __attribute__((always_inline)) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][1][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+      for (int i = 0; i < RG; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][1][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][1][i], acc[i][2 * qq + jj]);
+      for (int i = 0; i < RG; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][1][i], acc[i][2 * qq + jj]);
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
+      for (int i = 0; i < RG; ++i) acc[i][2 * qq + jj] = mfma16(fW[wset][0][jj], fA[aset][0][i], acc[i][2 * qq + jj]);
   };
   auto rescale = [&](int t) __attribute__((always_inline)) {
     if (ASC && t > 0 && (t * BK) % CHUNK == 0) {
       const int c = (t * BK) / CHUNK;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < RG; ++i) {
         const int ep = (int)(signed char)(ex[i] >> (8 * (c - 1)));
         const int en = (int)(signed char)(ex[i] >> (8 * c));
         const float f = ldexpf(1.0f, ep - en);
@@ -325,7 +334,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       }
     }
   };
-  // quarter with n fragment reads spread between its 24 MFMAs (one per two MFMAs)
+  // quarter with n fragment reads spread between its 6 RG MFMAs (one per two MFMAs)
   auto sched_reads = [&](auto NR) __attribute__((always_inline)) {
     constexpr int nr = decltype(NR)::value;
 #pragma unroll
@@ -333,7 +342,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 24 - 2 * nr, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6 * RG - 2 * nr, 0);
   };
 
   // prologue (issue order W0 A0 A1 W1 A2): tile 0 landed when 12 glds remain
@@ -422,17 +431,18 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     read_A(a ^ 1, t + 1);  // past the end: reads stale stages (never used)
     read_W(0, t + 1, 0);
     mfq(a, 1, 3);
+    // 6 RG MFMAs: 8 beside the operand loads, 2 RG + 4 beside the fragment reads, the rest (RG = 4: 4) alone
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
       __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
     }
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
+    for (int k = 0; k < 2 * RG + 4; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+    if constexpr (4 * RG > 12) __builtin_amdgcn_sched_group_barrier(0x008, 4 * RG - 12, 1);
     __builtin_amdgcn_s_setprio(0);
   };
   for (int t = 0; t < nk; t += 2) {  // nk = K / 32 is even (K = 512, 768)
@@ -444,10 +454,12 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   if (g.trace) tmain = rtime();
 
   // row scale of the last A chunk (edge layer 2)
-  float rs[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  float rs[RG];
+#pragma unroll
+  for (int i = 0; i < RG; ++i) rs[i] = 1.0f;
   if (ASC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
+    for (int i = 0; i < RG; ++i) rs[i] = ldexpf(1.0f, (int)(signed char)(ex[i] >> (8 * (K / CHUNK - 1))));
   }
   const int cw = n0 + wn * 128 + 4 * g4;  // this lane's first output column (+ 16 j)
 
@@ -467,7 +479,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
 
   if ((EPI == EPI_EDGE || EPI == EPI_SEGMEAN) && (g.dbg & 16)) {  // (profiling: main loop only)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < RG; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
@@ -708,7 +720,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
         bbv[(j + 1) & 1] = *reinterpret_cast<const f32x4*>(g.bias + cw + 16 * (j + 1));
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < RG; ++i)
 #pragma unroll
         for (int e = 0; e < 4; e += 2) {
           const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
@@ -722,17 +734,17 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           acc[i][j][e + 1] = x.y;
         }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[i][j])::"memory");
+      for (int i = 0; i < RG; ++i) asm volatile("" : "+v"(acc[i][j])::"memory");
     }
     if (!ONE) stamp(4);
     for (int half = 0; half < 2; ++half) {
       if (half == 1 && !ONE) stamp(5);
       if (wn == half) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < RG; ++i)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            *reinterpret_cast<f32x4*>(T + (wm * 64 + 16 * i + l16) * SEG_TP + 16 * j + 4 * g4) = acc[i][j];
+            *reinterpret_cast<f32x4*>(T + (wm * RW + 16 * i + l16) * SEG_TP + 16 * j + 4 * g4) = acc[i][j];
       }
       if (half == 0 && tid < nn) info[tid] = my;
       // LDS-only barriers in this loop: a __syncthreads() fence would also wait for the agg stores and
@@ -872,6 +884,13 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
 template <int EPI, bool ASC>
 __global__ __launch_bounds__(512, 1) void k_edge16(EdgeArgs g) {
   edge16_tile<EPI, ASC>(g, blockIdx.x, gridDim.x);
+}
+
+// Edge layer 2 on 192-row tiles (3 row groups per wave: three quarters of a 256-row tile's MFMAs and epilogue):
+// the second launch of a mixed row tiling, whose 256-row tiles fill whole rounds of the CUs and whose short tiles
+// take the partial last round (runtime.hip short_row_tiles)
+__global__ __launch_bounds__(512, 1) void k_edge16_short(EdgeArgs g) {
+  edge16_tile<EPI_SEGMEAN, true, false, 3>(g, blockIdx.x, gridDim.x);
 }
 
 // Edge layer 1's partial last round and edge layer 2 in one grid: blocks [0, nb1) are layer-1 tiles
@@ -1620,8 +1639,8 @@ hipError_t edge_gemm16_pairs_layer(const EdgeArgs& g1, const EdgeArgs& g2, const
     return hipErrorInvalidValue;
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.rtiles || !g2.sbuf || !g2.msgbuf || !g2.rcnt || !g2.agg ||
       !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags ||
-      (long)g2.ntiles != ps.R || (long)g2.ntiles * BM < g2.E)
-    return hipErrorInvalidValue;
+      (long)g2.ntiles != ps.R || (long)g2.ntiles * BM < g2.E || g2.rt_first || g2.rt_count || g2.rt_h || g2.rt_e0)
+    return hipErrorInvalidValue;  // (uniform 256-row tiles only)
   if (!ps.jobs || !ps.pflag || ps.jstride < 1 || ps.npx < 1) return hipErrorInvalidValue;
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   hipLaunchKernelGGL(k_edge16_pairs_grid, dim3((unsigned)(8 * ps.jstride)), dim3(512), LDS_B, s, g1, g2, ps);
@@ -1646,7 +1665,8 @@ static hipError_t edge16_init_once() {
                       (const void*)k_edge16<EPI_SEGMEAN, true>, (const void*)k_edge16<EPI_STD, true>,
                       (const void*)k_edge16_tail, (const void*)k_edge16_layer, (const void*)k_edge16_layer_dyn,
                       (const void*)k_edge16_repair<EPI_EDGE, false>, (const void*)k_edge16_repair<EPI_SEGMEAN, true>,
-                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_grid, (const void*)k_edge16_pairs_repair};
+                      (const void*)k_edge16_pairs, (const void*)k_edge16_pairs_grid, (const void*)k_edge16_pairs_repair,
+                      (const void*)k_edge16_short};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_B);
     if (e != hipSuccess) return e;
@@ -1677,9 +1697,9 @@ hipError_t edge_gemm16_tail(const EdgeArgs& g1, const EdgeArgs& g2, int repair_g
       !g2.xbad)
     return hipErrorInvalidValue;
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.tiles || g2.ntiles < 1 || !g2.agg || !g2.bias ||
-      !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale ||
+      !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.rt_first || g2.rt_count || g2.rt_h || g2.rt_e0 ||
       (g2.rtiles && (!g2.sbuf || !g2.msgbuf || !g2.rcnt || (long)g2.ntiles * BM < g2.E)))
-    return hipErrorInvalidValue;
+    return hipErrorInvalidValue;  // (uniform tiles only)
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   const long nt1 = ((g1.M - g1.row_base + BM - 1) / BM) * (g1.N / BN);
   const long nb1 = (nt1 + 7) / 8 * 8;
@@ -1731,8 +1751,8 @@ hipError_t edge_gemm16_layer(const EdgeArgs& g1, const EdgeArgs& g2, int lag, in
   if (g2.N != H || g2.K % CHUNK || g2.K / CHUNK > 4 || !g2.rtiles || !g2.sbuf || !g2.msgbuf || !g2.rcnt || !g2.agg ||
       !g2.bias || !g2.aexp || !g2.node_n || !g2.A || !g2.W || !g2.wscale || g2.flags || g2.lflags != g1.lflags ||
       g2.npairs != g1.npairs || (long)g2.ntiles * BM < g2.E || (long)g2.ntiles * BM - g2.E >= BM || g1.M != g1.E ||
-      lag < 1)
-    return hipErrorInvalidValue;
+      lag < 1 || g2.rt_first || g2.rt_count || g2.rt_h || g2.rt_e0)
+    return hipErrorInvalidValue;  // (uniform 256-row tiles only)
   if (hipError_t e = edge16_init(); e != hipSuccess) return e;
   const long R = g2.ntiles;
   if (sched) {  // persistent, the last rows claimed at run time (k_edge16_layer_dyn)
@@ -1763,10 +1783,26 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
   const bool asc = g.aexp != nullptr;
   if (asc && (g.K % CHUNK || g.K / CHUNK > 4)) return hipErrorInvalidValue;
   long blocks;
+  bool short_tiles = false;
   if (epi == EPI_SEGMEAN) {
     if (g.N != H || !g.tiles || !g.agg || !g.bias || !asc || !g.node_n) return hipErrorInvalidValue;
-    if (g.rtiles && (!g.sbuf || !g.msgbuf || !g.rcnt || (long)g.ntiles * BM < g.E)) return hipErrorInvalidValue;
-    blocks = (long)g.ntiles * g.npairs * (g.N / BN);
+    long nt = g.ntiles;
+    if (g.rtiles) {
+      if (!g.sbuf || !g.msgbuf || !g.rcnt) return hipErrorInvalidValue;
+      if (g.rt_first || g.rt_count || g.rt_h || g.rt_e0) {
+        // one launch of a mixed tiling: tiles [rt_first, rt_first + rt_count) of ntiles, each with at least one row
+        nt = g.rt_count;
+        if ((g.rt_h != 0 && g.rt_h != BM && g.rt_h != kShortRows) || g.rt_first < 0 || nt < 1 ||
+            g.rt_first + nt > g.ntiles || g.rt_e0 < 0 || g.rt_e0 + (nt - 1) * (g.rt_h ? g.rt_h : BM) >= g.E)
+          return hipErrorInvalidValue;
+        short_tiles = g.rt_h == kShortRows;
+      } else if ((long)g.ntiles * BM < g.E) {
+        return hipErrorInvalidValue;
+      }
+    } else if (g.rt_first || g.rt_count || g.rt_h || g.rt_e0) {
+      return hipErrorInvalidValue;
+    }
+    blocks = nt * g.npairs * (g.N / BN);
   } else {
     if (g.M <= g.row_base || g.row_base < 0) return hipErrorInvalidValue;
     if (epi == EPI_EDGE &&
@@ -1779,6 +1815,8 @@ hipError_t edge_gemm16(const EdgeArgs& g, int epi, hipStream_t s) {
   const dim3 grid((unsigned)blocks), block(512);
   if (epi == EPI_EDGE)
     hipLaunchKernelGGL((k_edge16<EPI_EDGE, false>), grid, block, LDS_B, s, ga);
+  else if (epi == EPI_SEGMEAN && short_tiles)
+    hipLaunchKernelGGL(k_edge16_short, grid, block, LDS_B, s, ga);
   else if (epi == EPI_SEGMEAN)
     hipLaunchKernelGGL((k_edge16<EPI_SEGMEAN, true>), grid, block, LDS_B, s, ga);
   else if (asc)

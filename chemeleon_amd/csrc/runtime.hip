@@ -89,6 +89,9 @@ struct chm_model {
                          // half its matrix work; both directions' S from one GEMM row), then edge layer 2
   int edge_pairs_layer = 1;  // CHM_EDGE_PAIRS_LAYER / option edge_pairs_layer: both edge layers on pairs in one
                              // static grid (k_edge16_pairs_grid) from edge_layer_min row tiles on; 0 = two launches
+  int edge_rows_short = 1;   // CHM_EDGE_ROWS_SHORT / option edge_rows_short: batches below edge_layer_min row tiles whose
+                             // last round of 256-row tiles is at most 3/4 full take that round as 192-row tiles
+                             // (short_row_tiles, set at batch creation; bit-identical)
   int ncu = 0;          // compute units of the device the model lives on
   int device = 0;        // its HIP device ordinal (the current device at chm_model_create)
   unsigned xcd_mask = 0; // XCC ids a grid's blocks ran on at model creation (the persistent edge kernel needs 0xff)
@@ -127,6 +130,8 @@ struct chm_batch {
   int2* rinfo = nullptr;    // per row tile: its node list (EdgeArgs::rinfo), and its length
   int* rinfo_n = nullptr;
   long nrt = 0, r2tot = 0;  // row tiles; rows of the nodes continued from a previous tile
+  // a mixed row tiling (short_row_tiles): tiles [0, rt_nbig) have 256 rows, the rest kShortRows; -1 = all 256
+  long rt_nbig = -1;
   float *sbuf = nullptr, *msgbuf = nullptr;
   unsigned* rcnt = nullptr;
   unsigned* lflags = nullptr;  // k_edge16_layer: per row tile (returns to 0 at the end of every launch)
@@ -339,6 +344,8 @@ extern "C" int chm_model_create(const chm_dims* dims, const float* const* p, int
     if (pairs) m->edge_pairs = atoi(pairs);
     const char* player = getenv("CHM_EDGE_PAIRS_LAYER");
     if (player) m->edge_pairs_layer = atoi(player);
+    const char* rshort = getenv("CHM_EDGE_ROWS_SHORT");
+    if (rshort) m->edge_rows_short = atoi(rshort);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&m->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       m->ncu = 0;
@@ -492,6 +499,10 @@ extern "C" int chm_model_set_option(chm_model* m, const char* key, int64_t value
     m->edge_pairs_layer = value != 0;
     return CHM_OK;
   }
+  if (k == "edge_rows_short") {  // short last-round row tiles for the batches created from now on (bit-identical)
+    m->edge_rows_short = value != 0;
+    return CHM_OK;
+  }
   if (k == "edge_lag") {
     if (value < 1 || value > kMaxLag) return fail(CHM_E_ARG, "edge_lag must be in [1, 1000]");
     m->edge_lag = (int)value;
@@ -554,6 +565,7 @@ struct BatchTables {
   std::vector<int2> rinfo;   // fc: the row tiles' node lists (EdgeArgs::rinfo, kRowInfo per tile)
   std::vector<int> rinfo_n;
   long nrt = 0, r2tot = 0;
+  long rt_nbig = -1;  // fc: 256-row tiles before the kShortRows ones (-1: all 256 rows; set before batch_fill)
   long N = 0, E = 0;  // knn: E = the edge capacity
   // fc: the unordered pairs i <= j of every crystal, row-major (edge layer 1 on pairs, k_edge16_pairs)
   std::vector<int> pi, pj;
@@ -593,20 +605,28 @@ static int batch_tables(const int32_t* h_natoms, int B, BatchTables& t, const Ba
   return CHM_OK;
 }
 
+// Row-tile geometry: tiles [0, nbig) of 256 rows, then tiles of kShortRows (nbig < 0: all 256 rows)
+static long rt_count(long E, long nbig) {
+  return nbig < 0 ? (E + kTileRows - 1) / kTileRows : nbig + (E - nbig * kTileRows + kShortRows - 1) / kShortRows;
+}
+static long rt_start(long k, long nbig) {
+  return nbig < 0 || k <= nbig ? k * kTileRows : nbig * kTileRows + (k - nbig) * kShortRows;
+}
+
 // Row tiles of an fc batch (edge rows grouped by source node; node v's rows [estart, estart + n)):
-// tile t = rows [256 t, 256 t + 256), {first node starting in it, first node starting after it, the
-// node that began in tile t-1 and continues here (-1: none), the offset of those continued rows in
+// tile t = rows [256 t, 256 t + 256) (a mixed tiling: rt_start), {first node starting in it, first node starting
+// after it, the node that began in tile t-1 and continues here (-1: none), the offset of those continued rows in
 // msgbuf}. Returns the continued rows' total (msgbuf rows per conditioning); out null: sizing only.
 static long row_tiles(const BatchTables& t, std::vector<int4>* out) {
-  const long E = t.E, nrt = (E + kTileRows - 1) / kTileRows;
+  const long E = t.E, nrt = rt_count(E, t.rt_nbig), nb = t.rt_nbig;
   if (out) out->assign(nrt, make_int4((int)t.N, (int)t.N, -1, 0));
   long r2tot = 0, tc = 0, node = 0;
   long prev_end = 0;  // end row of the previous node
   for (size_t g = 0; g < t.nat.size(); ++g)
     for (int i = 0; i < t.nat[g]; ++i, ++node) {
       const long es = t.eoff[g] + (long)i * t.nat[g];
-      for (; tc < nrt && tc * kTileRows <= es; ++tc) {  // tiles starting in (previous start, es]
-        const long s0 = tc * kTileRows;
+      for (; tc < nrt && rt_start(tc, nb) <= es; ++tc) {  // tiles starting in (previous start, es]
+        const long s0 = rt_start(tc, nb);
         int4 r = make_int4((int)node, (int)t.N, -1, 0);
         if (node > 0 && prev_end > s0 && s0 < es) {  // node-1 began before the tile and reaches into it
           r.z = (int)(node - 1);
@@ -618,7 +638,7 @@ static long row_tiles(const BatchTables& t, std::vector<int4>* out) {
       prev_end = es + t.nat[g];
     }
   for (; tc < nrt; ++tc) {  // tiles after the last node start (the last node's rest)
-    const long s0 = tc * kTileRows;
+    const long s0 = rt_start(tc, nb);
     int4 r = make_int4((int)t.N, (int)t.N, -1, 0);
     if (prev_end > s0) {
       r.z = (int)(t.N - 1);
@@ -642,7 +662,7 @@ static void row_tile_nodes(BatchTables& t) {
   t.rinfo_n.assign(nrt, 0);
   for (long k = 0; k < nrt; ++k) {
     const int4 rt = t.rtiles[k];
-    const long e0 = k * kTileRows, e1 = e0 + (E - e0 < kTileRows ? E - e0 : kTileRows);
+    const long e0 = rt_start(k, t.rt_nbig), e1 = std::min<long>(E, rt_start(k + 1, t.rt_nbig));
     const int nreg = rt.y - rt.x;
     const bool head = nreg > 0 && t.estart[rt.y - 1] + t.nn[rt.y - 1] > e1;
     const bool cont = rt.z >= 0;
@@ -738,6 +758,30 @@ static long count_tiles(const BatchTables& t) {
       rows += t.nat[g];
     }
   return n;
+}
+
+// A mixed row tiling for edge layer 2 (r6). Below edge_layer_min row tiles edge layer 2 runs on the
+// two-launch schedule, where a last round of 256-row tiles may leave CUs idle (64x20: 400 tiles on 256 CUs, the second
+// round 56% full). When that round is at most 3/4 full, its rows fit one round of 192-row tiles, which cost ~3/4 of a
+// 256-row tile: tiles [0, nbig) fill whole rounds with 256 rows (one launch), the rest run on kShortRows rows
+// (k_edge16_short, a second launch). Returns nbig, or -1 for the uniform tiling. A cut node's sum stays one sequential
+// sum over its edges across tile ends, so every output is bit-identical to the uniform tiling's.
+static long short_row_tiles(const BatchTables& t, int P, long ncu, long layer_min) {
+  if (t.knn || t.E <= 0 || ncu <= 0 || P < 1) return -1;
+  const long R = (t.E + kTileRows - 1) / kTileRows;
+  if (R >= layer_min) return -1;  // (the one-grid schedules take uniform tiles)
+  for (int n : t.nat)
+    if (n > kShortRows) return -1;  // (a node then spans at most two tiles)
+  const long J = 2L * P, per = ncu / J;  // jobs per row tile (conditionings x column tiles); row tiles per round
+  if (per < 1) return -1;
+  const long rounds = (R * J + ncu - 1) / ncu;
+  const long nbig = (rounds - 1) * per;
+  if (rt_count(t.E, nbig) - nbig > per) return -1;  // more than one round of short tiles
+  return nbig;
+}
+static long short_row_tiles(const BatchTables& t, const chm_model* m, int P) {
+  if (m->math != MATH_SPLIT16 || !m->edge_rows_short || !m->edge_rows) return -1;
+  return short_row_tiles(t, P, m->ncu, m->edge_layer_min);
 }
 
 // carves every device buffer of `b` from `base` (null: sizing pass); returns the bytes used
@@ -837,6 +881,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   BatchTables t;
   int rc = batch_tables(h_natoms, B, t, bo);
   if (rc) return rc;
+  t.rt_nbig = short_row_tiles(t, m, max_pairs);
   batch_fill(t);
   chm_batch* b = new chm_batch();
   b->m = m;
@@ -853,8 +898,9 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
   b->ntiles = t.knn ? (int)(t.N + 1) : (int)t.tiles.size();
   b->nrt = t.knn ? 0 : t.nrt;
   b->r2tot = t.knn ? 0 : t.r2tot;
+  b->rt_nbig = t.knn ? -1 : t.rt_nbig;
   b->Ep = t.knn ? 0 : t.Ep;
-  if (!t.knn && b->math == MATH_SPLIT16 && t.E > 0) {
+  if (!t.knn && b->math == MATH_SPLIT16 && t.E > 0 && t.rt_nbig < 0) {  // (the pair grid: uniform row tiles)
     pair_plan(t.nat, t.E, t.Ep, t.nrt, b->P, m->edge_lag, b->pplan);
     if (!pair_plan_ok(b->pplan)) {
       delete b;
@@ -878,7 +924,7 @@ static int batch_build(const chm_model* m, const int32_t* h_natoms, int B, int m
      // Only for a short partial round (<= 1/4 of the CUs): 64x40 (32 of 256 tiles) gains 6% per step;
      // at 256x40 (128 of 256) the split grid lost 0.8% (profiles/r2/split_*)
     const long tiles1 = (t.E + kTileRows - 1) / kTileRows * (H / 256);
-    if (!t.knn && m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu && (tiles1 % m->ncu) * 4 <= m->ncu) {
+    if (!t.knn && t.rt_nbig < 0 && m->ncu > 0 && tiles1 > m->ncu && tiles1 % m->ncu && (tiles1 % m->ncu) * 4 <= m->ncu) {
       long full = tiles1 / m->ncu * m->ncu;
       full -= full % (H / 256);
       const long rows_a = full / (H / 256) * kTileRows;
@@ -945,12 +991,14 @@ extern "C" int chm_debug_layer_seq(int64_t n, int P, int lag, int64_t* out) {
   return CHM_OK;
 }
 
-extern "C" int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2, int64_t cap2, int32_t* counts,
-                                   int64_t cap) {
+extern "C" int chm_debug_row_nodes_ex(const int32_t* h_natoms, int B, int64_t nbig, int32_t* out2, int64_t cap2,
+                                      int32_t* counts, int64_t cap) {
   if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   BatchTables t;
   int rc = batch_tables(h_natoms, B, t);
   if (rc) return rc;
+  if (nbig >= 0 && nbig * kTileRows >= t.E) return fail(CHM_E_ARG, "nbig: no short tile left");
+  t.rt_nbig = nbig < 0 ? -1 : nbig;
   batch_fill(t);
   const long R = (long)t.rtiles.size();
   if (out2 && cap2 >= 2 * (int64_t)t.rinfo.size())
@@ -963,11 +1011,19 @@ extern "C" int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2
   return (int)R;
 }
 
-extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
+extern "C" int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2, int64_t cap2, int32_t* counts,
+                                   int64_t cap) {
+  return chm_debug_row_nodes_ex(h_natoms, B, -1, out2, cap2, counts, cap);
+}
+
+extern "C" int chm_debug_row_tiles_ex(const int32_t* h_natoms, int B, int64_t nbig, int32_t* out4, int64_t cap4,
+                                      int64_t* r2tot) {
   if (!h_natoms || B < 1) return fail(CHM_E_ARG, "bad batch arguments");
   BatchTables t;
   int rc = batch_tables(h_natoms, B, t);
   if (rc) return rc;
+  if (nbig >= 0 && nbig * kTileRows >= t.E) return fail(CHM_E_ARG, "nbig: no short tile left");
+  t.rt_nbig = nbig < 0 ? -1 : nbig;
   std::vector<int4> rt;
   const long r2 = row_tiles(t, &rt);
   if (r2tot) *r2tot = r2;
@@ -976,6 +1032,25 @@ extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4
       out4[4 * k] = rt[k].x; out4[4 * k + 1] = rt[k].y; out4[4 * k + 2] = rt[k].z; out4[4 * k + 3] = rt[k].w;
     }
   return (int)rt.size();
+}
+
+extern "C" int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t cap4, int64_t* r2tot) {
+  return chm_debug_row_tiles_ex(h_natoms, B, -1, out4, cap4, r2tot);
+}
+
+// the mixed row tiling short_row_tiles chooses for a batch (256-row tiles before the short ones, -1: uniform)
+extern "C" int64_t chm_debug_short_row_tiles(const int32_t* h_natoms, int B, int P, int ncu, int64_t layer_min) {
+  if (!h_natoms || B < 1 || P < 1 || P > 2) return fail(CHM_E_ARG, "bad batch arguments");
+  BatchTables t;
+  int rc = batch_tables(h_natoms, B, t);
+  if (rc) return rc;
+  return short_row_tiles(t, P, ncu, layer_min);
+}
+
+// the row tiling of a batch as it was created (256-row tiles before the short ones, -1: uniform)
+extern "C" int64_t chm_batch_short_row_tiles(const chm_batch* b) {
+  if (!b) return fail(CHM_E_ARG, "batch is NULL");
+  return b->rt_nbig;
 }
 
 extern "C" int chm_batch_create(const chm_model* m, const int32_t* h_natoms, int B, int max_pairs, chm_batch** out) {
@@ -1002,10 +1077,11 @@ extern "C" size_t chm_batch_workspace_bytes_ex(const chm_model* m, const int32_t
   b.knn = bo.knn;
   b.C_cap = t.C;
   if (!t.knn) {
-    b.nrt = (t.E + kTileRows - 1) / kTileRows;
+    t.rt_nbig = short_row_tiles(t, m, max_pairs);
+    b.nrt = rt_count(t.E, t.rt_nbig);
     b.r2tot = row_tiles(t, nullptr);
     b.Ep = t.Ep;
-    if (b.math == MATH_SPLIT16 && t.E > 0) pair_plan(t.nat, t.E, t.Ep, b.nrt, b.P, m->edge_lag, b.pplan);
+    if (b.math == MATH_SPLIT16 && t.E > 0 && t.rt_nbig < 0) pair_plan(t.nat, t.E, t.Ep, b.nrt, b.P, m->edge_lag, b.pplan);
   }
   return batch_layout(&b, m, nullptr, count_tiles(t));
 }
@@ -1301,7 +1377,8 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
   // the memsets cost 4.8 us each per call, 0.9% of a 64x20 step)
   // both edge layers on pairs in one grid (k_edge16_pairs_grid) for this call
   const bool pair_grid = pairs && m->edge_pairs_layer && m->edge_rows && b->rtiles && m->edge_layer && b->psched &&
-                         P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu;
+                         P == b->P && b->nrt >= m->edge_layer_min && m->ncu > 0 && m->xcd_mask == 0xffu &&
+                         b->rt_nbig < 0;
   const bool waits = !pairs || pair_grid;
   // the pair grid's repair requests and per-layer flags start clear in every call: zeroed by the embedding launch
   // below (two memset nodes less per call)
@@ -1391,6 +1468,22 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         e2.rinfo = b->rinfo; e2.rinfo_n = b->rinfo_n;
         e2.rcnt = b->rcnt; e2.r2tot = b->r2tot;
       }
+      // edge layer 2 on the two-launch schedule: one launch, or on a mixed row tiling (short_row_tiles) its 256-row
+      // tiles, then its 192-row tiles (k_edge16_short)
+      auto layer2 = [&](const EdgeArgs& ga) -> hipError_t {
+        if (!ga.rtiles || b->rt_nbig < 0) return edge_gemm16(ga, EPI_SEGMEAN, s);
+        if (b->rt_nbig > 0) {
+          EdgeArgs gb = ga;
+          gb.rt_count = (int)b->rt_nbig;
+          if (hipError_t r = edge_gemm16(gb, EPI_SEGMEAN, s); r != hipSuccess) return r;
+        }
+        EdgeArgs gs = ga;
+        gs.rt_first = (int)b->rt_nbig;
+        gs.rt_count = (int)(b->nrt - b->rt_nbig);
+        gs.rt_h = kShortRows;
+        gs.rt_e0 = b->rt_nbig * kTileRows;
+        return edge_gemm16(gs, EPI_SEGMEAN, s);
+      };
       // (instrumented eager launches keep one launch per layer, so the per-kernel timings stay whole;
       // captured launches are never instrumented)
       hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -1423,8 +1516,9 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
           HIPCHK(edge_gemm16_pairs(e1p, s));
         }
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
-        HIPCHK(edge_gemm16(e2, EPI_SEGMEAN, s));
-      } else if (e2.rtiles && m->edge_layer && b->nrt >= m->edge_layer_min && (!m->edge_trace || m->edge_trace_layer == 3)) {
+        HIPCHK(layer2(e2));
+      } else if (e2.rtiles && m->edge_layer && b->nrt >= m->edge_layer_min && b->rt_nbig < 0 &&
+                 (!m->edge_trace || m->edge_trace_layer == 3)) {
         // both layers in one grid: layer 2's row tiles behind layer 1's (k_edge16_layer)
         e1.lflags = e2.lflags = b->lflags;
         e1.xbad = e2.xbad = b->xbad + l;
@@ -1466,7 +1560,7 @@ static int run_decoder(chm_batch* b, int P, const int64_t* a, const float* x, co
         }
         ProfScope ps(CHM_K_EDGE_MESSAGE, s);
         HIPCHK(traced_edge_launch(m, e2, 2, E, s, [&] {
-          return edge_gemm16(e2, EPI_SEGMEAN, s);
+          return layer2(e2);
         }));
       }
     } else {

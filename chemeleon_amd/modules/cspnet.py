@@ -222,9 +222,11 @@ class CSPNet(nn.Module):
             _lib.check(_lib.load().chm_model_set_option(self.hip_model().handle, key.encode(), int(value)),
                        "chm_model_set_option")
             self._options[key] = int(value)
-            # (a batch carves the pre-split operand buffers only when created with node_ps, and plans its
-            # pair-grid job lists with the edge_lag of its creation: cached batches are rebuilt)
-            if key in ("node_ps", "edge_lag"):
+            # (a batch carves the pre-split operand buffers only when created with node_ps, plans its
+            # pair-grid job lists with the edge_lag of its creation and picks its row tiling (short last-round
+            # tiles or the one-grid schedules' uniform ones) from the options of its creation: cached batches
+            # are rebuilt)
+            if key in ("node_ps", "edge_lag", "edge_layer_min", "edge_rows_short", "edge_rows"):
                 self._batches.clear()
 
     def set_math(self, mode: str):

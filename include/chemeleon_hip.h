@@ -341,6 +341,18 @@ int chm_debug_row_tiles(const int32_t* h_natoms, int B, int32_t* out4, int64_t c
 /* (host only) the row tiles' node lists (EdgeArgs::rinfo: kRowInfo = 260 {node, packed} pairs per tile) and
  * their lengths, as edge layer 2's segment-mean epilogue reads them; returns the number of row tiles */
 int chm_debug_row_nodes(const int32_t* h_natoms, int B, int32_t* out2, int64_t cap2, int32_t* counts, int64_t cap);
+/* The same two on a mixed row tiling (r6): tiles [0, nbig) of 256 edge rows, then tiles of 192 rows (nbig < 0: the
+ * uniform tiling; CHM_E_ARG when the 256-row tiles leave no row). A batch takes such a tiling at creation when edge
+ * layer 2 runs on the two-launch schedule (fewer than the option edge_layer_min row tiles, crystals of at most 192
+ * atoms, split16, option edge_rows_short on) and its last round of 256-row tiles would be at most 3/4 full: that
+ * round's rows then run as one round of 192-row tiles (k_edge16_short, a launch of their own). Bit-identical.
+ * chm_debug_short_row_tiles: the nbig a batch of these crystals takes for P conditionings on a device of ncu CUs with
+ * edge_layer_min = layer_min (-1: uniform); chm_batch_short_row_tiles: the one a created batch took. */
+int chm_debug_row_tiles_ex(const int32_t* h_natoms, int B, int64_t nbig, int32_t* out4, int64_t cap4, int64_t* r2tot);
+int chm_debug_row_nodes_ex(const int32_t* h_natoms, int B, int64_t nbig, int32_t* out2, int64_t cap2, int32_t* counts,
+                           int64_t cap);
+int64_t chm_debug_short_row_tiles(const int32_t* h_natoms, int B, int P, int ncu, int64_t layer_min);
+int64_t chm_batch_short_row_tiles(const chm_batch* b);
 /* Host-only test hook: the block -> job map of the one-grid edge-layer kernel (k_edge16_layer) for R
  * row tiles, P conditionings and layer-2 lag `lag`. Returns the grid size nb (or a negative CHM_E_*);
  * if out holds >= 2 nb int64 it receives per block {kind (0 none, 1 edge layer 1, 2 edge layer 2),

@@ -9,6 +9,7 @@ Tolerances (north star: 1e-4 relative fp32, atom types bit-exact):
 * lattices: rtol 1e-4 (absolute floor 1e-4 x max |lattice|).
 """
 
+import ctypes
 import numpy as np
 import pytest
 import torch
@@ -974,3 +975,38 @@ def test_pair_epilogue_staged_rows_are_bit_identical(cn, nat):
     for k, name in ((1, "two launches, staged"), (2, "pair grid, staged")):
         for u, v, what in zip(outs[0], outs[k], ("types", "frac", "lattice")):
             assert torch.equal(u, v), f"{what}: {name} differs from the unstaged pair epilogue"
+
+
+@pytest.mark.parametrize("nat,nowait", [([20] * 64, 0), ([20] * 64, 1), ([6] * 4, 0), ([20] * 30, 0),
+                                        ([190, 37, 5, 1, 80, 2, 64, 100], 0), ([190, 37, 5, 1, 80, 2, 64, 100], 1)])
+def test_short_row_tiles_are_bit_identical(cn, nat, nowait):
+    """Mixed row tiling (r6): a batch below edge_layer_min row tiles whose last round of 256-row tiles is at most 3/4
+    full runs edge layer 2 as its 256-row tiles, then 192-row tiles (k_edge16_short) for that round's rows. A node cut
+    at a tile end stays one sequential sum over its edges (published partial sum, or the continued rows through
+    msgbuf: 'edge_rows_nowait'), so one reverse step equals the uniform tiling ('edge_rows_short' 0) bit for bit.
+    Shapes: configs[1] (64 tiles of 256 + 48 of 192), all-short tilings of one partial round, and a ragged batch with
+    a 190-atom crystal (nodes longer than half a short tile, cut at 256 / 192 boundaries)."""
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(29)
+    a0 = torch.randint(0, 100, (N,), generator=g)
+    x0 = torch.rand(N, 3, generator=g)
+    l0 = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    nz = (torch.rand((N, 104), generator=g), torch.randn(B, 3, 3, generator=g), torch.randn(N, 3, generator=g),
+          torch.randn(N, 3, generator=g))
+    lib = _lib.load()
+    arr = (ctypes.c_int32 * B)(*nat)
+    want = lib.chm_debug_short_row_tiles(arr, B, 2, torch.cuda.get_device_properties(0).multi_processor_count, 256)
+    assert want >= 0, "the shape should take a mixed tiling"
+    model = _model(1000)
+    model.decoder.set_option("edge_rows_nowait", nowait)
+    outs, took = [], []
+    for short in (0, 1):
+        model.decoder.set_option("edge_rows_short", short)
+        outs.append([o.cpu() for o in model.reverse_step(500, a0, x0, l0, nat, 2.0, 1e-5, cn[0], cn[1], noise=nz)])
+        took.append([lib.chm_batch_short_row_tiles(b.handle) for b in model.decoder._batches.values()])
+    del model
+    torch.cuda.empty_cache()
+    assert took[0] and all(t == -1 for t in took[0])
+    assert took[1] and all(t == want for t in took[1]), (took[1], want)
+    for u, v, what in zip(outs[0], outs[1], ("types", "frac", "lattice")):
+        assert torch.equal(u, v), f"{what}: the mixed row tiling differs from the uniform one"
