@@ -157,14 +157,18 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   }
   const int K = g.K, nk = K / BK;
   const unsigned long long t0 = g.trace ? rtime() : 0;  // (profiling: CHM_EDGE_TRACE block timelines)
+  // (dbg 4096 with a trace: slots 4 / 5 = the shader clock counter at the block's start / end instead of the epilogue
+  // markers, for the block's mean clock: tools/trace_summary.py --clock)
+  const unsigned long long c0 = g.trace && (g.dbg & 4096) ? ctime() : 0;
   unsigned long long tmain = 0;
   auto stamp = [&](int slot) __attribute__((always_inline)) {
-    if (g.trace && tid == 0) g.trace[6 * vb + slot] = rtime();
+    if (g.trace && tid == 0 && !(g.dbg & 4096)) g.trace[6 * vb + slot] = rtime();
   };
   auto stamp_end = [&]() __attribute__((always_inline)) {
     if (g.trace && tid == 0) {
       unsigned long long* o = g.trace + 6 * vb;
       o[0] = hwid(); o[1] = t0; o[2] = tmain; o[3] = rtime();
+      if (g.dbg & 4096) { o[4] = c0; o[5] = ctime(); }
     }
   };
 

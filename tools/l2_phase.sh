@@ -5,5 +5,5 @@ for d in ${DBGS:-0 4}; do
   CHM_EDGE_DBG=$d CHM_EDGE_PAIRS=0 CHM_EDGE_LAYER=0 CHM_EDGE_TRACE_LAYER=2 CHM_EDGE_TRACE=$O/t_$d.bin timeout -k 10 240 \
     python bench.py --steps 1 --warmup 1 --no-graph --no-cpu-baseline --no-api-legs --no-traffic "$@" > $O/b_$d.log 2>&1 ||
     { tail -20 $O/b_$d.log; exit 1; }
-  echo "== dbg $d"; python tools/trace_summary.py $O/t_$d.bin
+  echo "== dbg $d"; python tools/trace_summary.py $O/t_$d.bin ${SUMARGS:-}
 done
