@@ -1010,3 +1010,31 @@ def test_short_row_tiles_are_bit_identical(cn, nat, nowait):
     assert took[1] and all(t == want for t in took[1]), (took[1], want)
     for u, v, what in zip(outs[0], outs[1], ("types", "frac", "lattice")):
         assert torch.equal(u, v), f"{what}: the mixed row tiling differs from the uniform one"
+
+
+def test_short_row_tiles_single_conditioning_bit_identical(cn):
+    """The mixed row tiling with one conditioning (a plain decoder call, max_pairs = 1: 2 jobs per row tile): 30
+    crystals of 20 atoms take 63 tiles of 192 rows in one round; the decoder outputs equal the uniform tiling's."""
+    nat = [20] * 30
+    B, N = len(nat), sum(nat)
+    g = torch.Generator().manual_seed(31)
+    a = torch.randint(0, 104, (N,), generator=g)
+    x = torch.rand(N, 3, generator=g)
+    lat = torch.eye(3).expand(B, 3, 3) * 4.0 + 0.3 * torch.randn(B, 3, 3, generator=g)
+    model = _model(1000)
+    te = model.time_embed(torch.full((B,), 700, dtype=torch.long)).to(DEV)
+    nat_t = torch.tensor(nat)
+    lib = _lib.load()
+    outs, took = [], []
+    for short in (0, 1):
+        model.decoder.set_option("edge_rows_short", short)
+        o = model.decoder(atom_types=a.to(DEV), frac_coords=x.to(DEV), lattices=lat.to(DEV), num_atoms=nat_t.to(DEV),
+                          node2graph=torch.arange(B).repeat_interleave(nat_t).to(DEV), t=te,
+                          text_embeds=cn[0].expand(B, -1).to(DEV))
+        outs.append([o.node_features.cpu(), o.atom_types_out.cpu(), o.coords_out.cpu(), o.lattice_out.cpu()])
+        took.append([lib.chm_batch_short_row_tiles(b.handle) for b in model.decoder._batches.values()])
+    del model
+    torch.cuda.empty_cache()
+    assert took[0] == [-1] and took[1] == [0], took
+    for u, v, what in zip(outs[0], outs[1], ("nodes", "types", "coords", "lattice")):
+        assert torch.equal(u, v), f"{what}: the mixed row tiling differs from the uniform one"
