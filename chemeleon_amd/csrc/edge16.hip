@@ -40,6 +40,12 @@ constexpr bool kSegTable = CHM_SEG_TABLE;
 #define CHM_GRID_TRACE 0
 #endif
 constexpr bool kGridTrace = CHM_GRID_TRACE;
+// K-loop ablations of A/B builds only (CHM_BUILD_DEFS=-DCHM_LOOP_ABL=n; wrong results, read in cycles): bit 0 = no
+// per-K-tile s_barrier, 1 = no vmcnt waits, 2 = no operand loads in the loop, 3 = no lgkmcnt waits before the quarters
+#ifndef CHM_LOOP_ABL
+#define CHM_LOOP_ABL 0
+#endif
+constexpr bool kAblBar = CHM_LOOP_ABL & 1, kAblVm = CHM_LOOP_ABL & 2, kAblLd = CHM_LOOP_ABL & 4, kAblLgkm = CHM_LOOP_ABL & 8;
 
 namespace {
 
@@ -397,19 +403,19 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
   auto tile = [&](int t, auto CUR) __attribute__((always_inline)) {
     constexpr int a = decltype(CUR)::value;
     rescale(t);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
     __builtin_amdgcn_s_setprio(1);
     read_W(1, t, 1);
     mfq(a, 0, 0);
     sched_reads(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
     read_W(0, t, 2);
     mfq(a, 1, 1);
     sched_reads(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
     read_W(1, t, 3);
     mfq(a, 0, 2);
@@ -418,16 +424,18 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     // this wave is done reading tile t; this thread's part of tile t+1 has landed (only A(t+2) may
     // still be in flight; near the end everything is waited for); after the barrier everyone's
     // has, and tile t's stages are free
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (t < nk - 2)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblVm) {
+      if (t < nk - 2)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!kAblBar) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if (t + 2 < nk) issueW(t + 2);  // (nothing is loaded past the end of K)
-    if (t + 3 < nk) issueA(t + 3);
+    if (t + 2 < nk && !kAblLd) issueW(t + 2);  // (nothing is loaded past the end of K)
+    if (t + 3 < nk && !kAblLd) issueA(t + 3);
     if (EPI == EPI_EDGE && pre) {
       if (t == nk - 2) stage_rows(0, 0);
       if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
@@ -1247,19 +1255,19 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
 
   auto tile = [&](f32x4 (&acc)[2][8], int t, auto CUR) __attribute__((always_inline)) {
     constexpr int a = decltype(CUR)::value;
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): A_t and W_t quarter 0 are in
     __builtin_amdgcn_s_setprio(1);
     read_W(1, t, 1);
     mfq(acc, a, 0, 0);
     sched_reads(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
     read_W(0, t, 2);
     mfq(acc, a, 1, 1);
     sched_reads(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_setprio(1);
     read_W(1, t, 3);
     mfq(acc, a, 0, 2);
@@ -1267,16 +1275,18 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
     __builtin_amdgcn_s_setprio(0);
     // this wave is done reading tile t; this thread's part of tile t+1 has landed (only A(t+2) may still
     // be in flight: 2 glds; near the end everything is waited for); after the barrier everyone's has
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (t < nk - 2)
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!kAblVm) {
+      if (t < nk - 2)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (!kAblBar) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if (t + 2 < nk) issueW(t + 2);
-    if (t + 3 < nk) issueA(t + 3);
+    if (t + 2 < nk && !kAblLd) issueW(t + 2);
+    if (t + 3 < nk && !kAblLd) issueA(t + 3);
     read_A(a ^ 1, t + 1);  // past the end: reads stale stages (never used)
     read_W(0, t + 1, 0);
     mfq(acc, a, 1, 3);
