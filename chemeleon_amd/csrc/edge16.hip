@@ -46,6 +46,15 @@ constexpr bool kGridTrace = CHM_GRID_TRACE;
 #define CHM_LOOP_ABL 0
 #endif
 constexpr bool kAblBar = CHM_LOOP_ABL & 1, kAblVm = CHM_LOOP_ABL & 2, kAblLd = CHM_LOOP_ABL & 4, kAblLgkm = CHM_LOOP_ABL & 8;
+// Branch-free K loops (r6): every K-tile issues its operand loads (past the end of K they re-read the last tile into the
+// stage just freed) and waits with one vmcnt, so the tile body is one basic block and its sched_group_barrier
+// interleaving of loads and MFMAs takes effect (conditional loads were a block of their own, issued as a burst).
+// Not for the directed layer-1 tiles (EPI_EDGE), whose last K-tiles stage P / Q rows into the A ring.
+// (A/B builds: -DCHM_LOOP_UNI=0 restores the conditional form)
+#ifndef CHM_LOOP_UNI
+#define CHM_LOOP_UNI 1
+#endif
+constexpr bool kLoopUni = CHM_LOOP_UNI;
 
 namespace {
 
@@ -425,8 +434,9 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     // still be in flight; near the end everything is waited for); after the barrier everyone's
     // has, and tile t's stages are free
     if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
+    constexpr bool uni = kLoopUni && EPI != EPI_EDGE;
     if (!kAblVm) {
-      if (t < nk - 2)
+      if (uni || t < nk - 2)
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -434,8 +444,8 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
     if (!kAblBar) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if (t + 2 < nk && !kAblLd) issueW(t + 2);  // (nothing is loaded past the end of K)
-    if (t + 3 < nk && !kAblLd) issueA(t + 3);
+    if ((uni || t + 2 < nk) && !kAblLd) issueW(t + 2);  // (uni: past the end of K, a re-read of the last tile)
+    if ((uni || t + 3 < nk) && !kAblLd) issueA(t + 3);
     if (EPI == EPI_EDGE && pre) {
       if (t == nk - 2) stage_rows(0, 0);
       if (t == nk - 1 && g.npairs > 1) stage_rows(1, PRE_ROW1);
@@ -1277,7 +1287,7 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
     // be in flight: 2 glds; near the end everything is waited for); after the barrier everyone's has
     if (!kAblLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
     if (!kAblVm) {
-      if (t < nk - 2)
+      if (kLoopUni || t < nk - 2)
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1285,8 +1295,8 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
     if (!kAblBar) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if (t + 2 < nk && !kAblLd) issueW(t + 2);
-    if (t + 3 < nk && !kAblLd) issueA(t + 3);
+    if ((kLoopUni || t + 2 < nk) && !kAblLd) issueW(t + 2);
+    if ((kLoopUni || t + 3 < nk) && !kAblLd) issueA(t + 3);
     read_A(a ^ 1, t + 1);  // past the end: reads stale stages (never used)
     read_W(0, t + 1, 0);
     mfq(acc, a, 1, 3);
