@@ -55,6 +55,13 @@ constexpr bool kAblBar = CHM_LOOP_ABL & 1, kAblVm = CHM_LOOP_ABL & 2, kAblLd = C
 #define CHM_LOOP_UNI 1
 #endif
 constexpr bool kLoopUni = CHM_LOOP_UNI;
+// The pair epilogue's profiling ablations (CHM_EDGE_DBG 4 no stores, 131072 / 262144 reverse-direction store variants,
+// 524288 P / Q rows not loaded, 2097152 no exponent bytes) in A/B builds only (-DCHM_PAIR_ABL=1): as runtime tests in
+// the product they cost the epilogue a zero-fill and a branch around every P / Q read (r6)
+#ifndef CHM_PAIR_ABL
+#define CHM_PAIR_ABL 0
+#endif
+constexpr bool kPairAbl = CHM_PAIR_ABL;
 
 namespace {
 
@@ -1378,7 +1385,7 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
   }
   _Float16* S0 = reinterpret_cast<_Float16*>(g.S);
   const bool odd = l16 & 1;
-  const bool nostore = g.dbg & 4;  // (profiling)
+  const bool nostore = kPairAbl && (g.dbg & 4);  // (profiling)
   const float* T = reinterpret_cast<const float*>(lds);
   auto conditioning = [&](int c, auto STG) __attribute__((always_inline)) {
     constexpr bool staged = decltype(STG)::value;
@@ -1401,11 +1408,11 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
         }
         // (dbg 131072 / 262144, profiling: no reverse-direction stores / the reverse rows stored at the forward
         // rows' places: what the scattered reverse rows cost; wrong results)
-        const long orow = (long)c * g.E + (dir && !(g.dbg & 262144) ? pe[i].y : pe[i].x);
-        const bool st = ok[i] && !nostore && (dir == 0 || (ni[i] != nj[i] && !(g.dbg & 131072)));
+        const long orow = (long)c * g.E + (dir && !(kPairAbl && (g.dbg & 262144)) ? pe[i].y : pe[i].x);
+        const bool st = ok[i] && !nostore && (dir == 0 || (ni[i] != nj[i] && !(kPairAbl && (g.dbg & 131072))));
         f32x4 v[8];
         float mx = 0.f;
-        const bool nopq = g.dbg & 524288;  // (profiling: P / Q rows not loaded; wrong results)
+        const bool nopq = kPairAbl && (g.dbg & 524288);  // (profiling: P / Q rows not loaded; wrong results)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const f32x4 pv = nopq ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(prow + 16 * j);
@@ -1454,7 +1461,7 @@ __device__ __forceinline__ void pair_tile(const EdgeArgs& g, long bid, int tid_i
           if (st_e) *reinterpret_cast<f16x8*>(se + cc * 64) = odd ? r8 : hv;  // even lane's row: hi (even), lo (odd)
           if (st_o) *reinterpret_cast<f16x8*>(so + cc * 64) = odd ? lv : r8;  // odd lane's row
         }
-        if (st && g4 == 0 && !(g.dbg & 2097152)) {  // (dbg 2097152, profiling: no exponent bytes; wrong results)
+        if (st && g4 == 0 && !(kPairAbl && (g.dbg & 2097152))) {  // (dbg 2097152, profiling: no exponent bytes; wrong results)
           signed char* px = reinterpret_cast<signed char*>(g.sexp) + orow * 4 + (n0 + wn * 128) / CHUNK;
           *px = (signed char)ex2;
         }

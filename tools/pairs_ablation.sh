@@ -1,7 +1,9 @@
 # Edge layer 1 on pairs (k_edge16_pairs): where its time goes. CHM_EDGE_DBG (profiling only, wrong results):
 # 0 = product, 16 = main loops only (both edge kernels), 4 = no epilogue stores, 131072 = no reverse-row
 # stores, 262144 = reverse rows stored at the forward rows' places, 524288 = P / Q rows not loaded (zeros),
-# 1048576 = P / Q rows read from global memory (not staged in LDS; exact), 2097152 = no exponent-byte stores. Runs the
+# 1048576 = P / Q rows read from global memory (not staged in LDS; exact), 2097152 = no exponent-byte stores (from r6
+# the pair epilogue's bits 4, 131072, 262144, 524288, 2097152 need an A/B build, CHM_BUILD_DEFS=-DCHM_PAIR_ABL=1, loaded
+# with CHM_LIB; and wall times of data-changing variants carry a clock change: tools/grid_ablation_cycles.sh). Runs the
 # two-launch schedule (CHM_EDGE_PAIRS_LAYER=0) so that edge layer 1 has a launch of its own. Run from the repo root on
 # the GPU box: bash tools/pairs_ablation.sh <tag> [bench args]
 TAG=$1; shift
