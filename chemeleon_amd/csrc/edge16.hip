@@ -62,6 +62,12 @@ constexpr bool kLoopUni = CHM_LOOP_UNI;
 #define CHM_PAIR_ABL 0
 #endif
 constexpr bool kPairAbl = CHM_PAIR_ABL;
+// (edge layer 2's SiLU ablation select, dbg 8: compiled in only by A/B builds -DCHM_L2_SEL=1; r6 same-box A/B without it
+// 512x40 50.87 -> 50.71 ms per step, 64x40 7.37 -> 7.31, 64x20 2.647 -> 2.625, bit-identical: profiles/r6/l2_sel/)
+#ifndef CHM_L2_SEL
+#define CHM_L2_SEL 0
+#endif
+constexpr bool kL2Sel = CHM_L2_SEL;
 
 namespace {
 
@@ -755,10 +761,9 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           const f32x2e a2 = {acc[i][j][e], acc[i][j][e + 1]};
           const f32x2e s2 = f32x2e{scv[j & 1][e], scv[j & 1][e + 1]} * rs[i];
           const f32x2e y = a2 * s2 + f32x2e{bbv[j & 1][e], bbv[j & 1][e + 1]};
-          // (dbg 8: profiling. Removing this uniform select from the epilogue made edge layer 2 ~3% slower
-          // under the compiler's schedule, profiles/r2/layer/epilogue_select_ab.txt, so it stays; the
-          // layer-1 epilogue's copy was removed: -14% VALU instructions in k_edge16<1>)
-          const f32x2e x = (g.dbg & 8) ? y : silu_e2(y);
+          // (dbg 8, profiling, A/B builds only: in r2 removing this uniform select made edge layer 2 ~3% slower
+          // under the compiler's schedule, profiles/r2/layer/epilogue_select_ab.txt; in r6 its removal gains)
+          const f32x2e x = (kL2Sel && (g.dbg & 8)) ? y : silu_e2(y);
           acc[i][j][e] = x.x;
           acc[i][j][e + 1] = x.y;
         }
