@@ -55,9 +55,10 @@ constexpr bool kAblBar = CHM_LOOP_ABL & 1, kAblVm = CHM_LOOP_ABL & 2, kAblLd = C
 #define CHM_LOOP_UNI 1
 #endif
 constexpr bool kLoopUni = CHM_LOOP_UNI;
-// The pair epilogue's profiling ablations (CHM_EDGE_DBG 4 no stores, 131072 / 262144 reverse-direction store variants,
-// 524288 P / Q rows not loaded, 2097152 no exponent bytes) in A/B builds only (-DCHM_PAIR_ABL=1): as runtime tests in
-// the product they cost the epilogue a zero-fill and a branch around every P / Q read (r6)
+// The epilogues' profiling ablations (CHM_EDGE_DBG 4 no stores, 131072 / 262144 reverse-direction store variants,
+// 524288 P / Q rows not loaded, 2097152 no exponent bytes; edge layer 2: 4 no agg stores, 32 no segment sums) in A/B
+// builds only (-DCHM_PAIR_ABL=1): as runtime tests in the product they cost the pair epilogue a zero-fill and a
+// branch around every P / Q read (r6)
 #ifndef CHM_PAIR_ABL
 #define CHM_PAIR_ABL 0
 #endif
@@ -812,14 +813,14 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
           lo[1] = (_Float16)(x1 - (float)hi[1]);
           const long row = (long)seg_c * g.nnodes + node;
           _Float16* o16 = reinterpret_cast<_Float16*>(g.aggs) + row * (2 * H) + (gcol >> 4) * 32 + (gcol & 15);
-          if (!(g.dbg & 4)) {
+          if (!(kPairAbl && (g.dbg & 4))) {
             *reinterpret_cast<f16x2s*>(o16) = hi;
             *reinterpret_cast<f16x2s*>(o16 + 16) = lo;
             if (lane == 0) reinterpret_cast<signed char*>(g.agge)[row * 4 + (gcol >> 7)] = (signed char)ex;
           }
           return;
         }
-        if (!(g.dbg & 4)) *reinterpret_cast<f32x2e*>(g.agg + ((long)seg_c * g.nnodes + node) * H + gcol) = mean;
+        if (!(kPairAbl && (g.dbg & 4))) *reinterpret_cast<f32x2e*>(g.agg + ((long)seg_c * g.nnodes + node) * H + gcol) = mean;
         if (g.agg_max) {  // the node row's max |agg| for the split16 node GEMM reading it
           float m = fmaxf(fabsf(mean.x), fabsf(mean.y));
 #pragma unroll
@@ -829,7 +830,7 @@ __device__ __forceinline__ void edge16_tile(const EdgeArgs& g, long vb, long nvb
       };
       // row tiles: one counter per (conditioning, boundary tile, column half)
       const int cidx = (n0 / BN) * 4 + half * 2;
-      for (int k = tid >> 6; k < nn && !(g.dbg & 32); k += 8) {  // (dbg 32: profiling, no sums)
+      for (int k = tid >> 6; k < nn && !(kPairAbl && (g.dbg & 32)); k += 8) {  // (dbg 32: profiling, no sums)
         const int2 nk = info[k];
         const int4 ni = {nk.y & 1023, (nk.y >> 10) & 1023, nk.x, nk.y >> 20};  // {rows, first row, node, kind}
         const float* src = T + ni.y * SEG_TP + col;
