@@ -57,6 +57,12 @@ static_assert(3 * STB<true> * NST<true, 3> <= 160 * 1024, "LDS");
 static_assert(3 * STB<true, 64> * NST<true, 3, 64> <= 160 * 1024 && 4 * STB<true, 64> * NST<true, 4, 64> <= 160 * 1024, "LDS");
 static_assert(STB<false, 64> * NST<false, 2, 64> <= NODE_LDS, "LDS");  // bf16x3 64-row tiles, two blocks per CU
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// K-loop ablations of A/B builds only (-DCHM_NODE_ABL=n; wrong results, read in cycles): bit 0 = no per-K-step barrier,
+// 1 = no operand loads in the loop, 2 = no A split (one conversion instead: the VAR 1 probe in every kernel)
+#ifndef CHM_NODE_ABL
+#define CHM_NODE_ABL 0
+#endif
+constexpr bool kNAblBar = CHM_NODE_ABL & 1, kNAblLd = CHM_NODE_ABL & 2, kNAblSplit = CHM_NODE_ABL & 4;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
         for (int e = 0; e < 8; e += 2) {
           const f32x2 x = (e < 4 ? f32x2{ra0[i][e], ra0[i][e + 1]} : f32x2{ra1[i][e - 4], ra1[i][e - 3]}) * asc[i];
           const f16x2 hi = __builtin_convertvector(x, f16x2);
-          const f16x2 lo = VAR == 1 ? hi : __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
+          const f16x2 lo = (VAR == 1 || kNAblSplit) ? hi : __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
           fa[set][0][i][e] = hi[0]; fa[set][0][i][e + 1] = hi[1];
           fa[set][1][i][e] = lo[0]; fa[set][1][i][e + 1] = lo[1];
         }
@@ -419,9 +425,9 @@ __global__ __launch_bounds__(256, NB) void k_node_gemm(GemmArgs g) {
     // this thread's part of tile t+1 has landed (AHEAD - 2 tiles may stay in flight)
     vm_wait<(AHEAD - 2) * GL>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();                     // everyone's; tile t's stage has been read
+    if (!kNAblBar) __builtin_amdgcn_s_barrier();      // everyone's; tile t's stage has been read
     asm volatile("" ::: "memory");
-    issue(t + AHEAD);                                 // into tile t's stage; past the end: re-reads
+    if (!kNAblLd) issue(t + AHEAD);                   // into tile t's stage; past the end: re-reads
     __builtin_amdgcn_s_setprio(1);
     read_raw(t + 1, cur ^ 1);                         // past the end: reads a re-read tile
     if constexpr (S16) {
