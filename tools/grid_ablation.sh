@@ -1,6 +1,8 @@
 # Pair grid (k_edge16_pairs_grid, the default schedule): launch time under CHM_EDGE_DBG ablations (profiling only,
 # wrong results): 0 product, 4 no epilogue stores, 16 main loops only, 524288 pair P / Q rows not loaded,
-# 4194304 pair jobs publish without waiting for their S stores (the drain). Repo root, GPU box:
+# 4194304 pair jobs publish without waiting for their S stores (the drain). From r6 the epilogue bits (4, 524288) need
+# an A/B build (CHM_BUILD_DEFS=-DCHM_PAIR_ABL=1, loaded with CHM_LIB), and wall times of data-changing variants carry a
+# clock change: read them in cycles (tools/grid_ablation_cycles.sh). Repo root, GPU box:
 #   bash tools/grid_ablation.sh <tag> [bench args]
 TAG=$1; shift
 O=gpurun_out/$TAG

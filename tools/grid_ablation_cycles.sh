@@ -2,6 +2,7 @@
 # data the kernels see (e.g. S never written), and the chip's clock follows the data (MI355X_MICROARCH.md, DVFS), so
 # a wall-time difference alone can be a clock artifact. One rocprofv3 pass per variant, GRBM_GUI_ACTIVE (summed over
 # the 8 XCDs) per dispatch + the kernel trace; repo root, GPU box: bash tools/grid_ablation_cycles.sh <tag> [bench args]
+# (from r6 the epilogue bits 4 and 524288 act only in an A/B build: CHM_BUILD_DEFS=-DCHM_PAIR_ABL=1, run with CHM_LIB)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
